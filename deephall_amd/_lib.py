@@ -1,0 +1,117 @@
+"""ctypes binding of the C ABI declared in include/deephall_amd.h.
+
+The HIP library is the only compute path: if it is missing this module raises —
+there is no CPU / PyTorch fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdeephall_amd.so"
+
+DH_NSTATS = 16
+STAT_NAMES = [
+    "energy_re",
+    "energy_im",
+    "clipped_re",
+    "clipped_im",
+    "ere2",
+    "kinetic_re",
+    "kinetic_im",
+    "potential",
+    "angular_momentum_z",
+    "angular_momentum_z_square",
+    "angular_momentum_square",
+    "pmove",
+    "nvalid",
+]
+
+EXPORTS = [
+    "dh_create",
+    "dh_destroy",
+    "dh_last_error",
+    "dh_version",
+    "dh_param_layout",
+    "dh_set_params",
+    "dh_workspace_bytes",
+    "dh_logpsi",
+    "dh_mcmc_step",
+    "dh_local_energy",
+    "dh_energy_stats",
+    "dh_init_walkers",
+    "dh_potential",
+    "dh_debug_trunk",
+    "dh_debug_f_offset",
+]
+
+
+class DhConfig(C.Structure):
+    _fields_ = [
+        ("n_up", C.c_int),
+        ("n_dn", C.c_int),
+        ("flux", C.c_int),
+        ("radius", C.c_float),
+        ("interaction_strength", C.c_float),
+        ("interaction_type", C.c_int),
+        ("num_heads", C.c_int),
+        ("heads_dim", C.c_int),
+        ("num_layers", C.c_int),
+        ("ndets", C.c_int),
+        ("orbital_type", C.c_int),
+    ]
+
+
+_lib = None
+
+
+def load(path: Path | str | None = None):
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(
+            f"deephall_amd HIP library not found at {p}. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)."
+        )
+    lib = C.CDLL(str(p))
+    vp, sz, i32, u64, i64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64, C.c_int64
+    lib.dh_create.argtypes = [C.POINTER(DhConfig), C.POINTER(vp)]
+    lib.dh_create.restype = i32
+    lib.dh_destroy.argtypes = [vp]
+    lib.dh_destroy.restype = None
+    lib.dh_last_error.restype = C.c_char_p
+    lib.dh_version.restype = C.c_char_p
+    lib.dh_param_layout.argtypes = [vp, C.POINTER(sz), i32]
+    lib.dh_param_layout.restype = i32
+    lib.dh_set_params.argtypes = [vp, vp, sz, vp]
+    lib.dh_set_params.restype = i32
+    lib.dh_workspace_bytes.argtypes = [vp, i32, i32]
+    lib.dh_workspace_bytes.restype = sz
+    lib.dh_logpsi.argtypes = [vp, vp, i32, vp, vp, sz, vp]
+    lib.dh_logpsi.restype = i32
+    lib.dh_mcmc_step.argtypes = [vp, vp, vp, vp, i32, i32, C.c_float, u64, u64, i64, vp, vp, sz, vp]
+    lib.dh_mcmc_step.restype = i32
+    lib.dh_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, sz, vp]
+    lib.dh_local_energy.restype = i32
+    lib.dh_energy_stats.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]
+    lib.dh_energy_stats.restype = i32
+    lib.dh_init_walkers.argtypes = [vp, vp, i32, u64, i64, vp]
+    lib.dh_init_walkers.restype = i32
+    lib.dh_potential.argtypes = [vp, vp, i32, vp, vp]
+    lib.dh_potential.restype = i32
+    lib.dh_debug_trunk.argtypes = [vp, vp, i32, i32, vp, sz, vp]
+    lib.dh_debug_trunk.restype = i32
+    lib.dh_debug_f_offset.argtypes = [vp, i32, i32]
+    lib.dh_debug_f_offset.restype = sz
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().dh_last_error().decode(errors="replace")
+        raise RuntimeError(f"deephall_amd error {rc}: {msg}")

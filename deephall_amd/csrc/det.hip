@@ -1,0 +1,695 @@
+// Envelope contraction + batched complex slogdet + local-energy assembly.
+//
+// Orbital features F (output of the orbital GEMM, blocks.py:27-35) have rows
+// (walker, electron i, channel c) and columns ((blk*2+part)*M + m)*N*K + j*K + k.
+//   Phi_k[i][j] = sum_m F[i,m,j,k] env[i,m],  env = c_m u^(Q+m) v^(Q-m)   (blocks.py:64-68)
+//   log psi     = J + log sum_k exp(log det Phi_k)                       (psiformer.py:74-76, 91)
+// (exp(J/N) * Phi inside the determinant, psiformer.py:91, is added as J outside.)
+//
+// value kernel  (one 64-thread workgroup per walker): log psi only, LU with partial
+//               pivoting (|re|+|im| pivot choice, as LAPACK getrf).
+// energy kernel (one 256-thread workgroup per walker): channel determinants
+//   l_t  = tr(B Phi_t),  B = Phi0^-1 (Gauss-Jordan, partial pivoting)
+//   l_L  = tr(B Phi_L) - sum_t tr((B Phi_t)^2)
+//   l_Sk = tr(B Phi_Sk) - tr((B Phi_uk)^2),  Phi_uk = sum_t alpha_kt Phi_t
+// with Phi channels from the product rule of F and the envelope leaves, then
+// Jastrow, potential and the KE / Lz / Lz^2 / L^2 assembly (DESIGN.md §3.4,
+// equivalent to hamiltonian.py:115-169).
+#include "dh_internal.h"
+#include "device_common.h"
+
+namespace dh {
+namespace {
+
+__device__ inline float ipow(float b, int e) { return e < 0 ? 0.f : (e == 0 ? 1.f : powf(b, (float)e)); }
+
+// F element (complex) of row `row` at (blk, m, j, k)
+struct FView {
+  const float* F;
+  int ld, M, N, K;
+  __device__ inline cf at(size_t row, int blk, int m, int j, int k) const {
+    const size_t base = row * ld;
+    const int MNK = M * N * K;
+    const int off = m * N * K + j * K + k;
+    return cf{F[base + (size_t)(blk * 2) * MNK + off], F[base + (size_t)(blk * 2 + 1) * MNK + off]};
+  }
+};
+
+// envelope value (and optionally leaves) for electron angle (th, ph), harmonic index p
+struct EnvLeaf {
+  cf e0, dth, dph, lb, d2th;
+};
+__device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves) {
+  const int a = p, b = M - 1 - p;
+  const float m = 0.5f * (float)(a - b);
+  float c, s;
+  sincosf(0.5f * th, &s, &c);
+  float sph, cph;
+  sincosf(m * ph, &sph, &cph);
+  const float R = ipow(c, a) * ipow(s, b);
+  EnvLeaf L;
+  L.e0 = cf{norm * R * cph, norm * R * sph};
+  if (leaves) {
+    const float fa = (float)a, fb = (float)b;
+    const float R1 = 0.5f * (fb * ipow(c, a + 1) * ipow(s, b - 1) - fa * ipow(c, a - 1) * ipow(s, b + 1));
+    const float R2 = 0.25f * (fb * (fb - 1.f) * ipow(c, a + 2) * ipow(s, b - 2) - fb * (fa + 1.f) * R -
+                              fa * (fb + 1.f) * R + fa * (fa - 1.f) * ipow(c, a - 2) * ipow(s, b + 2));
+    float st, ct;
+    sincosf(th, &st, &ct);
+    L.dth = cf{norm * R1 * cph, norm * R1 * sph};
+    L.d2th = cf{norm * R2 * cph, norm * R2 * sph};
+    // d/dphi / sin th = i m e0 / st
+    L.dph = cf{-m * L.e0.im / st, m * L.e0.re / st};
+    // LB = d2th - m^2 e0 / st^2 + cot th * dth
+    const float cot = ct / st;
+    const float k2 = m * m / (st * st);
+    L.lb = cf{L.d2th.re - k2 * L.e0.re + cot * L.dth.re, L.d2th.im - k2 * L.e0.im + cot * L.dth.im};
+  }
+  return L;
+}
+
+// second derivative of the envelope along the rotation flow about axis k
+__device__ inline cf env_flow2(const cf& e0, const cf& dth, const cf& d2th, float m, float st, float ct, float sp,
+                               float cp, int k) {
+  const float cot = ct / st;
+  const float ph_hat[3] = {-sp, cp, 0.f};
+  const float th_hat[3] = {ct * cp, ct * sp, -st};
+  const float thp[3] = {cp * cot, sp * cot, -1.f};
+  const float dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.f};
+  const float dthp_dph[3] = {-sp * cot, cp * cot, 0.f};
+  const float cs[3] = {cp, sp, 0.f};
+  const float td = ph_hat[k];
+  const float pd = -th_hat[k] / st;
+  const float tdd = cs[k] * thp[k];
+  const float pdd = -(dthp_dth[k] * td - dthp_dph[k] * thp[k]);
+  // d_thph = i m dth ; d_phph = -m^2 e0 ; d_ph = i m e0
+  cf r;
+  r.re = d2th.re * td * td + 2.f * (-m * dth.im) * td * pd + (-m * m * e0.re) * pd * pd + dth.re * tdd +
+         (-m * e0.im) * pdd;
+  r.im = d2th.im * td * td + 2.f * (m * dth.re) * td * pd + (-m * m * e0.im) * pd * pd + dth.im * tdd +
+         (m * e0.re) * pdd;
+  return r;
+}
+
+// wave 0 finds the pivot row (first max of |re|+|im| in column p, rows >= p)
+__device__ inline void find_pivot(const cf* A, int lda, int N, int p, int* piv) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    float best = -1.f;
+    int bi = N;
+    for (int r = p + lane; r < N; r += 64) {
+      const float v = cabs1(A[r * lda + p]);
+      if (v > best) {
+        best = v;
+        bi = r;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (lane == 0) *piv = (bi < N) ? bi : p;
+  }
+}
+
+// In-place elimination on A [N][ncol] (lda) with partial pivoting.
+//   gj = true : Gauss-Jordan on an augmented [A | I] (ncol = 2N): right block -> A^-1
+//   gj = false: LU (rows below the pivot only) — determinant only
+// Accumulates log det into logdet (complex, phase unwrapped).  Uses __syncthreads.
+__device__ void eliminate(cf* A, int lda, int N, int ncol, bool gj, cf* fac, int* piv, cf* logdet) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) *logdet = cf{0.f, 0.f};
+  __syncthreads();
+  for (int p = 0; p < N; ++p) {
+    find_pivot(A, lda, N, p, piv);
+    __syncthreads();
+    const int pr = *piv;
+    if (pr != p) {
+      for (int c = tid; c < ncol; c += nt) {
+        const cf t = A[p * lda + c];
+        A[p * lda + c] = A[pr * lda + c];
+        A[pr * lda + c] = t;
+      }
+    }
+    __syncthreads();
+    const cf P = A[p * lda + p];
+    if (tid == 0) {
+      const float mag = sqrtf(P.re * P.re + P.im * P.im);
+      logdet->re += logf(mag);
+      logdet->im += atan2f(P.im, P.re) + (pr != p ? kPi : 0.f);
+    }
+    const cf Pinv = cdiv(cf{1.f, 0.f}, P);
+    __syncthreads();
+    if (gj) {
+      for (int r = tid; r < N; r += nt) fac[r] = (r == p) ? cf{0.f, 0.f} : A[r * lda + p];
+      for (int c = tid; c < ncol; c += nt) A[p * lda + c] = A[p * lda + c] * Pinv;
+    } else {
+      for (int r = tid; r < N; r += nt) fac[r] = (r > p) ? A[r * lda + p] * Pinv : cf{0.f, 0.f};
+    }
+    __syncthreads();
+    const int r0 = gj ? 0 : p + 1;
+    const int c0 = gj ? 0 : p;
+    const int nr = N - r0, nc = ncol - c0;
+    for (int idx = tid; idx < nr * nc; idx += nt) {
+      const int r = r0 + idx / nc, c = c0 + idx % nc;
+      if (r == p) continue;
+      const cf f = fac[r];
+      cf v = A[r * lda + c];
+      const cf a = A[p * lda + c];
+      v.re -= f.re * a.re - f.im * a.im;
+      v.im -= f.re * a.im + f.im * a.re;
+      A[r * lda + c] = v;
+    }
+    __syncthreads();
+  }
+}
+
+__device__ inline double jastrow_pair(double r, double al, double cst, double* f1, double* f2) {
+  const double ar = al + r;
+  *f1 = (cst * al * al) / (ar * ar);
+  *f2 = -2.0 * (cst * al * al) / (ar * ar * ar);
+  return -(cst * al * al) / ar;
+}
+
+// ------------------------------------------------------------------ value kernel
+__global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+                                 const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
+                                 int N, int n_up, int M, int K) {
+  extern __shared__ float sm_raw[];
+  cf* E0 = reinterpret_cast<cf*>(sm_raw);  // [N][M]
+  cf* A = E0 + N * M;                      // [N][N]
+  cf* fac = A + N * N;                     // [N]
+  cf* ld = fac + N;                        // [K] log dets
+  cf* logdet = ld + K;
+  int* piv = reinterpret_cast<int*>(logdet + 1);
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const FView F{Fp, ldF, M, N, K};
+  for (int idx = tid; idx < N * M; idx += nt) {
+    const int i = idx / M, p = idx % M;
+    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
+  }
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    for (int idx = tid; idx < N * N; idx += nt) {
+      const int i = idx / N, j = idx % N;
+      const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+      const size_t row = (size_t)b * N + i;
+      cf acc{0.f, 0.f};
+      for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
+      A[idx] = acc;
+    }
+    __syncthreads();
+    eliminate(A, N, N, N, false, fac, piv, logdet);
+    if (tid == 0) ld[k] = *logdet;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // log-sum-exp over determinants (psiformer.py:74-76)
+    float lmax = -INFINITY;
+    for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, ld[k].re);
+    float zr = 0.f, zi = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float mag = expf(ld[k].re - lmax);
+      zr += mag * cosf(ld[k].im);
+      zi += mag * sinf(ld[k].im);
+    }
+    float val_re = 0.5f * logf(zr * zr + zi * zi) + lmax;
+    float val_im = atan2f(zi, zr);
+    // Jastrow (blocks.py:76-121), chord distance on the unit sphere
+    double J = 0.0;
+    const double ap = jas[0], aa = jas[1];
+    for (int i = 0; i < N; ++i) {
+      const float ti = x[2 * (b * N + i)], pi_ = x[2 * (b * N + i) + 1];
+      const double xi = sin(ti) * cos(pi_), yi = sin(ti) * sin(pi_), zi_ = cos(ti);
+      for (int j = i + 1; j < N; ++j) {
+        const float tj = x[2 * (b * N + j)], pj = x[2 * (b * N + j) + 1];
+        const double dx = sin(tj) * cos(pj) - xi, dy = sin(tj) * sin(pj) - yi, dz = cos(tj) - zi_;
+        const double r = sqrt(dx * dx + dy * dy + dz * dz);
+        const bool same = (i < n_up) == (j < n_up);
+        double f1, f2;
+        J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+      }
+    }
+    logpsi[2 * b] = val_re + (float)J;
+    logpsi[2 * b + 1] = val_im;
+  }
+}
+
+// ------------------------------------------------------------------ energy kernel
+struct DetSmem {
+  int geo, alpha, E0, DTH, DPH, LB, D2TH, Aug, Binv, Phi, Mt, Mu, Gu, fac, ellt, ell0, ellL, ellS, red, misc, total;
+};
+__host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
+  // offsets in floats; complex arrays take 2 floats per element
+  DetSmem L;
+  const int T = 2 * N, NN = N * N;
+  int o = 0;
+  L.geo = o;
+  o += 4 * N;
+  L.alpha = o;
+  o += 3 * T;
+  o = (o + 1) & ~1;
+  L.E0 = o;
+  o += 2 * N * M;
+  L.DTH = o;
+  o += 2 * N * M;
+  L.DPH = o;
+  o += 2 * N * M;
+  L.LB = o;
+  o += 2 * N * M;
+  L.D2TH = o;
+  o += 2 * N * M;
+  L.Aug = o;
+  o += 2 * 2 * NN;
+  L.Binv = o;
+  o += 2 * NN;
+  L.Phi = o;
+  o += 2 * NN;
+  L.Mt = o;
+  o += 2 * NN;
+  L.Mu = o;
+  o += 3 * 2 * NN;
+  L.Gu = o;
+  o += 3 * 2 * NN;
+  L.fac = o;
+  o += 2 * N;
+  L.ellt = o;
+  o += 2 * K * T;
+  L.ell0 = o;
+  o += 2 * K;
+  L.ellL = o;
+  o += 2 * K;
+  L.ellS = o;
+  o += 2 * 3 * K;
+  L.red = o;
+  o += 4 * nwaves + 4;
+  L.misc = o;
+  o += 8;
+  L.total = o;
+  return L;
+}
+
+// block-wide sum of 4 floats, result returned to every thread (two __syncthreads)
+__device__ inline void block_sum4(float v[4], float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = wave_sum(v[q]);
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[4 * w + q] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[4 * i + q];
+    v[q] = s;
+  }
+  __syncthreads();
+}
+
+__global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+                                  const float* __restrict__ geo_g, const float* __restrict__ jas,
+                                  const float* __restrict__ norm, float* __restrict__ e_l, float* __restrict__ obs,
+                                  int N, int n_up, int M, int K, float Q, float radius, float lambda,
+                                  int interaction) {
+  extern __shared__ float sm[];
+  const int T = 2 * N, C = 2 * N + 5, NN = N * N;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const DetSmem L = det_layout(N, M, K, nt >> 6);
+  const int b = blockIdx.x;
+  float* geo = sm + L.geo;  // st ct sp cp
+  float* al = sm + L.alpha;
+  cf *E0 = (cf*)(sm + L.E0), *DTH = (cf*)(sm + L.DTH), *DPH = (cf*)(sm + L.DPH), *LBe = (cf*)(sm + L.LB),
+     *D2 = (cf*)(sm + L.D2TH);
+  cf *Aug = (cf*)(sm + L.Aug), *Binv = (cf*)(sm + L.Binv), *Phi = (cf*)(sm + L.Phi), *Mt = (cf*)(sm + L.Mt);
+  cf *Mu = (cf*)(sm + L.Mu), *Gu = (cf*)(sm + L.Gu), *fac = (cf*)(sm + L.fac);
+  cf *ellt = (cf*)(sm + L.ellt), *ell0 = (cf*)(sm + L.ell0), *ellL = (cf*)(sm + L.ellL), *ellS = (cf*)(sm + L.ellS);
+  float* red = sm + L.red;
+  int* piv = reinterpret_cast<int*>(sm + L.misc);
+  cf* logdet = reinterpret_cast<cf*>(sm + L.misc + 2);
+  const FView F{Fp, ldF, M, N, K};
+
+  for (int i = tid; i < N; i += nt) {
+    const float4 g = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
+    geo[4 * i] = g.x;
+    geo[4 * i + 1] = g.y;
+    geo[4 * i + 2] = g.z;
+    geo[4 * i + 3] = g.w;
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += nt) {
+    const int i = t >> 1;
+    const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((t & 1) == 0)
+        a = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+      else
+        a = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+      al[k * T + t] = a;
+    }
+  }
+  for (int idx = tid; idx < N * M; idx += nt) {
+    const int i = idx / M, p = idx % M;
+    const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true);
+    E0[idx] = e.e0;
+    DTH[idx] = e.dth;
+    DPH[idx] = e.dph;
+    LBe[idx] = e.lb;
+    D2[idx] = e.d2th;
+  }
+  __syncthreads();
+
+  const size_t rowbase = (size_t)b * N * C;  // row of (b, i, c) = rowbase + i*C + c
+  for (int kd = 0; kd < K; ++kd) {
+    // ---- Phi0 and its inverse (augmented Gauss-Jordan)
+    for (int idx = tid; idx < NN; idx += nt) {
+      const int i = idx / N, j = idx % N;
+      const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+      cf acc{0.f, 0.f};
+      for (int p = 0; p < M; ++p) cfma(acc, F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
+      Aug[i * 2 * N + j] = acc;
+      Aug[i * 2 * N + N + j] = (i == j) ? cf{1.f, 0.f} : cf{0.f, 0.f};
+    }
+    for (int idx = tid; idx < 3 * NN; idx += nt) {
+      Mu[idx] = cf{0.f, 0.f};
+      Gu[idx] = cf{0.f, 0.f};
+    }
+    __syncthreads();
+    eliminate(Aug, 2 * N, N, 2 * N, true, fac, piv, logdet);
+    for (int idx = tid; idx < NN; idx += nt) Binv[idx] = Aug[(idx / N) * 2 * N + N + idx % N];
+    if (tid == 0) ell0[kd] = *logdet;
+    __syncthreads();
+
+    float sum_trm2_re = 0.f, sum_trm2_im = 0.f;  // uniform across threads after block_sum4
+    // ---- tangent channels
+    for (int t = 0; t < T; ++t) {
+      const int it = t >> 1;
+      const cf* dE = (t & 1) ? DPH : DTH;
+      const float a0 = al[t], a1 = al[T + t], a2 = al[2 * T + t];
+      for (int idx = tid; idx < NN; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        const size_t rt = rowbase + (size_t)i * C + 1 + t;
+        const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+        const float phh[3] = {-sp, cp, 0.f};
+        const float thh[3] = {ct * cp, ct * sp, -st};
+        cf acc{0.f, 0.f}, g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
+        for (int p = 0; p < M; ++p) {
+          const cf f = F.at(rt, blk, p, j, kd);
+          const cf dth = DTH[i * M + p], dph = DPH[i * M + p];
+          cfma(acc, f, E0[i * M + p]);
+          cfma(g0, f, phh[0] * dth - thh[0] * dph);
+          cfma(g1, f, phh[1] * dth - thh[1] * dph);
+          cfma(g2, f, phh[2] * dth - thh[2] * dph);
+        }
+        if (i == it) {
+          const size_t r0 = rowbase + (size_t)i * C;
+          for (int p = 0; p < M; ++p) cfma(acc, F.at(r0, blk, p, j, kd), dE[i * M + p]);
+        }
+        Phi[idx] = acc;
+        Gu[idx] += a0 * g0;
+        Gu[NN + idx] += a1 * g1;
+        Gu[2 * NN + idx] += a2 * g2;
+      }
+      __syncthreads();
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int idx = tid; idx < NN; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        cf acc{0.f, 0.f};
+        for (int l = 0; l < N; ++l) cfma(acc, Binv[i * N + l], Phi[l * N + j]);
+        Mt[idx] = acc;
+        Mu[idx] += a0 * acc;
+        Mu[NN + idx] += a1 * acc;
+        Mu[2 * NN + idx] += a2 * acc;
+        if (i == j) {
+          v[0] += acc.re;
+          v[1] += acc.im;
+        }
+      }
+      __syncthreads();
+      for (int idx = tid; idx < NN; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        const cf prod = Mt[idx] * Mt[j * N + i];
+        v[2] += prod.re;
+        v[3] += prod.im;
+      }
+      block_sum4(v, red);
+      if (tid == 0) ellt[kd * T + t] = cf{v[0], v[1]};
+      sum_trm2_re += v[2];
+      sum_trm2_im += v[3];
+    }
+
+    // ---- Laplace-Beltrami channel
+    {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int idx = tid; idx < NN; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        const size_t r0 = rowbase + (size_t)i * C;
+        cf acc{0.f, 0.f}, acc2{0.f, 0.f};
+        for (int p = 0; p < M; ++p) {
+          cfma(acc, F.at(r0 + 1 + T, blk, p, j, kd), E0[i * M + p]);
+          cfma(acc, F.at(r0, blk, p, j, kd), LBe[i * M + p]);
+          cfma(acc2, F.at(r0 + 1 + 2 * i, blk, p, j, kd), DTH[i * M + p]);
+          cfma(acc2, F.at(r0 + 2 + 2 * i, blk, p, j, kd), DPH[i * M + p]);
+        }
+        acc += 2.f * acc2;
+        // tr(B Phi) = sum_ij B[j][i] Phi[i][j]
+        const cf pr = Binv[j * N + i] * acc;
+        v[0] += pr.re;
+        v[1] += pr.im;
+      }
+      block_sum4(v, red);
+      if (tid == 0) ellL[kd] = cf{v[0] - sum_trm2_re, v[1] - sum_trm2_im};
+    }
+    // ---- flow channels
+    for (int k = 0; k < 3; ++k) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int idx = tid; idx < NN; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        const size_t r0 = rowbase + (size_t)i * C;
+        const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+        cf acc{0.f, 0.f};
+        for (int p = 0; p < M; ++p) {
+          const float m = (float)p - 0.5f * (float)(M - 1);
+          const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
+          cfma(acc, F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
+          cfma(acc, F.at(r0, blk, p, j, kd), sf);
+        }
+        acc += 2.f * Gu[k * NN + idx];
+        const cf pr = Binv[j * N + i] * acc;
+        v[0] += pr.re;
+        v[1] += pr.im;
+        const cf m2 = Mu[k * NN + idx] * Mu[k * NN + j * N + i];
+        v[2] += m2.re;
+        v[3] += m2.im;
+      }
+      block_sum4(v, red);
+      if (tid == 0) ellS[3 * kd + k] = cf{v[0] - v[2], v[1] - v[3]};
+    }
+    __syncthreads();
+  }
+
+  // ---- combine determinants, Jastrow, potential, assembly (thread 0, double precision)
+  if (tid == 0) {
+    double lmax = -1e300;
+    for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
+    double wr[16], wi[16];
+    double zr = 0.0, zi = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double mag = exp((double)ell0[k].re - lmax);
+      wr[k] = mag * cos((double)ell0[k].im);
+      wi[k] = mag * sin((double)ell0[k].im);
+      zr += wr[k];
+      zi += wi[k];
+    }
+    const double zz = zr * zr + zi * zi;
+    for (int k = 0; k < K; ++k) {  // p_k = w_k / Z
+      const double pr = (wr[k] * zr + wi[k] * zi) / zz, pi_ = (wi[k] * zr - wr[k] * zi) / zz;
+      wr[k] = pr;
+      wi[k] = pi_;
+    }
+    const double val_re = 0.5 * log(zz) + lmax, val_im = atan2(zi, zr);
+    // g1_t and Laplacian combination
+    double tg_re[64], tg_im[64];
+    double LB_re = 0.0, LB_im = 0.0;
+    for (int k = 0; k < K; ++k) {
+      LB_re += wr[k] * ellL[k].re - wi[k] * ellL[k].im;
+      LB_im += wr[k] * ellL[k].im + wi[k] * ellL[k].re;
+    }
+    for (int t = 0; t < T; ++t) {
+      double gr = 0.0, gi = 0.0, sr = 0.0, si = 0.0;
+      for (int k = 0; k < K; ++k) {
+        const double lr = ellt[k * T + t].re, li = ellt[k * T + t].im;
+        gr += wr[k] * lr - wi[k] * li;
+        gi += wr[k] * li + wi[k] * lr;
+        const double l2r = lr * lr - li * li, l2i = 2.0 * lr * li;
+        sr += wr[k] * l2r - wi[k] * l2i;
+        si += wr[k] * l2i + wi[k] * l2r;
+      }
+      tg_re[t] = gr;
+      tg_im[t] = gi;
+      LB_re += sr - (gr * gr - gi * gi);
+      LB_im += si - 2.0 * gr * gi;
+    }
+    double S_re[3], S_im[3];
+    for (int kk = 0; kk < 3; ++kk) {
+      double a_r = 0.0, a_i = 0.0, m1r = 0.0, m1i = 0.0, m2r = 0.0, m2i = 0.0;
+      for (int k = 0; k < K; ++k) {
+        a_r += wr[k] * ellS[3 * k + kk].re - wi[k] * ellS[3 * k + kk].im;
+        a_i += wr[k] * ellS[3 * k + kk].im + wi[k] * ellS[3 * k + kk].re;
+        double gur = 0.0, gui = 0.0;
+        for (int t = 0; t < T; ++t) {
+          gur += (double)al[kk * T + t] * ellt[k * T + t].re;
+          gui += (double)al[kk * T + t] * ellt[k * T + t].im;
+        }
+        m1r += wr[k] * gur - wi[k] * gui;
+        m1i += wr[k] * gui + wi[k] * gur;
+        const double g2r = gur * gur - gui * gui, g2i = 2.0 * gur * gui;
+        m2r += wr[k] * g2r - wi[k] * g2i;
+        m2i += wr[k] * g2i + wi[k] * g2r;
+      }
+      S_re[kk] = a_r + m2r - (m1r * m1r - m1i * m1i);
+      S_im[kk] = a_i + m2i - 2.0 * m1r * m1i;
+    }
+    // Jastrow value, gradient (scaled basis) and Laplace-Beltrami; potential
+    double J = 0.0, Jlb = 0.0, pe = 0.0;
+    double Jg[64];
+    for (int t = 0; t < T; ++t) Jg[t] = 0.0;
+    const double ap = jas[0], aa = jas[1];
+    for (int i = 0; i < N; ++i) {
+      const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
+      const double ri[3] = {sti * cpi, sti * spi, cti};
+      const double thi[3] = {cti * cpi, cti * spi, -sti};
+      const double phi_[3] = {-spi, cpi, 0.0};
+      for (int j = i + 1; j < N; ++j) {
+        const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
+        const double rj[3] = {stj * cpj, stj * spj, ctj};
+        const double thj[3] = {ctj * cpj, ctj * spj, -stj};
+        const double phj[3] = {-spj, cpj, 0.0};
+        const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
+        const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
+        const bool same = (i < n_up) == (j < n_up);
+        double f1, f2;
+        J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+        const double gu = -f1 / r;
+        Jg[2 * i] += gu * (rj[0] * thi[0] + rj[1] * thi[1] + rj[2] * thi[2]);
+        Jg[2 * i + 1] += gu * (rj[0] * phi_[0] + rj[1] * phi_[1] + rj[2] * phi_[2]);
+        Jg[2 * j] += gu * (ri[0] * thj[0] + ri[1] * thj[1] + ri[2] * thj[2]);
+        Jg[2 * j + 1] += gu * (ri[0] * phj[0] + ri[1] * phj[1] + ri[2] * phj[2]);
+        Jlb += 2.0 * ((4.0 - r * r) * r * f2 + (4.0 - 3.0 * r * r) * f1) / (4.0 * r);
+        if (interaction == DH_INTERACTION_COULOMB)
+          pe += 1.0 / sqrt(2.0 - 2.0 * u);
+        else
+          pe += 1.0 + ((double)Q + 1.0) / (double)Q * u;
+      }
+    }
+    if (interaction == DH_INTERACTION_COULOMB) pe /= (double)radius;
+    pe *= (double)lambda;
+    LB_re += Jlb;
+    // assembly
+    double sq_re = 0.0, sq_im = 0.0, mag_re = 0.0, mag_im = 0.0;
+    for (int t = 0; t < T; ++t) {
+      tg_re[t] += Jg[t];
+      sq_re += tg_re[t] * tg_re[t] - tg_im[t] * tg_im[t];
+      sq_im += 2.0 * tg_re[t] * tg_im[t];
+    }
+    double Mv[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < N; ++i) {
+      const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+      const double cot = ct / st;
+      mag_re += (Q * cot) * (Q * cot);
+      // 2 i Q cot * t_phi_scaled
+      mag_re += -2.0 * Q * cot * tg_im[2 * i + 1];
+      mag_im += 2.0 * Q * cot * tg_re[2 * i + 1];
+      Mv[0] += Q * cp / st;
+      Mv[1] += Q * sp / st;
+    }
+    const double r2 = (double)radius * radius;
+    const double ke_re = (-LB_re - sq_re + mag_re) / (2.0 * r2);
+    const double ke_im = (-LB_im - sq_im + mag_im) / (2.0 * r2);
+    double G_re[3], G_im[3];
+    for (int kk = 0; kk < 3; ++kk) {
+      double gr = 0.0, gi = 0.0;
+      for (int t = 0; t < T; ++t) {
+        gr += (double)al[kk * T + t] * tg_re[t];
+        gi += (double)al[kk * T + t] * tg_im[t];
+      }
+      G_re[kk] = gr;
+      G_im[kk] = gi;
+    }
+    double L2 = 0.0;
+    for (int kk = 0; kk < 3; ++kk) {
+      // (G + i M)^2, real part
+      const double ar = G_re[kk], ai = G_im[kk] + Mv[kk];
+      L2 -= S_re[kk] + (ar * ar - ai * ai);
+    }
+    const double lz = G_im[2];
+    const double lz2 = -(S_re[2] + G_re[2] * G_re[2] - G_im[2] * G_im[2]);
+    e_l[2 * b] = (float)(ke_re + pe);
+    e_l[2 * b + 1] = (float)ke_im;
+    float* ob = obs + 8 * (size_t)b;
+    ob[0] = (float)ke_re;
+    ob[1] = (float)ke_im;
+    ob[2] = (float)pe;
+    ob[3] = (float)lz;
+    ob[4] = (float)lz2;
+    ob[5] = (float)L2;
+    ob[6] = (float)(val_re + J);
+    ob[7] = (float)val_im;
+  }
+}
+
+__global__ void potential_kernel(const float* __restrict__ x, float* __restrict__ pe, int nw, int N, float Q,
+                                 float radius, int interaction) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nw) return;
+  double acc = 0.0;
+  for (int i = 0; i < N; ++i) {
+    const double ti = x[2 * (b * N + i)], pi_ = x[2 * (b * N + i) + 1];
+    const double xi = sin(ti) * cos(pi_), yi = sin(ti) * sin(pi_), zi = cos(ti);
+    for (int j = i + 1; j < N; ++j) {
+      const double tj = x[2 * (b * N + j)], pj = x[2 * (b * N + j) + 1];
+      const double u = xi * sin(tj) * cos(pj) + yi * sin(tj) * sin(pj) + zi * cos(tj);
+      if (interaction == DH_INTERACTION_COULOMB)
+        acc += 1.0 / sqrt(2.0 - 2.0 * u);
+      else
+        acc += 1.0 + ((double)Q + 1.0) / (double)Q * u;
+    }
+  }
+  if (interaction == DH_INTERACTION_COULOMB) acc /= (double)radius;
+  pe[b] = (float)acc;
+}
+
+}  // namespace
+
+void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStream_t s) {
+  hipLaunchKernelGGL(potential_kernel, dim3((nw + 127) / 128), dim3(128), 0, s, x, pe, nw, d.N, d.Q, d.r,
+                     d.interaction);
+}
+
+void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
+                      float* logpsi, int nw, hipStream_t s) {
+  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4) * sizeof(float);
+  hipLaunchKernelGGL(det_value_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N,
+                     d.n_up, d.M, d.K);
+}
+
+void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
+                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s) {
+  const int threads = 256;
+  const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64);
+  ensure_smem(det_energy_kernel, (size_t)L.total * sizeof(float));
+  hipLaunchKernelGGL(det_energy_kernel, dim3(nw), dim3(threads), (size_t)L.total * sizeof(float), s, F, d.ld_orb, x,
+                     geo, jastrow, norm, e_l, obs, d.N, d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction);
+}
+
+size_t det_energy_smem_bytes(const Dims& d) { return (size_t)det_layout(d.N, d.M, d.K, 4).total * sizeof(float); }
+
+}  // namespace dh

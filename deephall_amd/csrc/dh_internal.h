@@ -1,0 +1,98 @@
+// Internal declarations shared by the HIP kernel files and the C ABI (api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/deephall_amd.h"
+
+namespace dh {
+
+// Static network geometry derived from dh_config (all sizes in elements).
+struct Dims {
+  int N, n_up, n_dn;   // electrons
+  int T;               // 2N first-order tangent channels
+  int C;               // 2N + 5 channels (local energy)
+  int M;               // 2Q + 1 monopole harmonics
+  float Q, r;          // monopole strength, sphere radius
+  int H, dh, D, L, K;  // heads, head dim, model dim, layers, determinants
+  int NB;              // spin blocks of the orbital layer (1 or 2)
+  int orb_cols;        // NB * 2 * M * N * K
+  int ld_orb;          // orb_cols rounded up to 128
+  int interaction;     // DH_INTERACTION_*
+  float lambda;        // interaction strength
+};
+
+// Device pointers into the packed parameter buffer.
+struct LayerParams {
+  const float *Wqkv, *bqkv, *Wol, *bol, *ln1, *Wm, *bm, *ln2;
+};
+struct Params {
+  const float* W0;
+  LayerParams layer[16];
+  const float *Worb, *borb, *jastrow;
+};
+
+// Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
+struct Pass {
+  int nw;      // walkers in this pass
+  int C;       // channels
+  int rows;    // nw * N * C
+  int rows_pad;
+};
+
+constexpr int kRowPad = 128;
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+template <typename Kern>
+inline void ensure_smem(Kern kernel, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+}
+
+// ---- kernel launchers (each .hip file) ----------------------------------------
+// gemm.hip: Y[r][n] = sum_k X[r][k] W[k][n] + (r % C == 0 ? bias[n] : 0) + (R ? R[r][n] : 0)
+void launch_gemm(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R, int ldr,
+                 float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+
+// input.hip
+// Features (psiformer.py:51-60) of every channel times W0 -> h [rows][D]; also
+// writes geo[nw][N][4] = (sin th, cos th, sin ph, cos ph).
+void launch_input(const Dims& d, const float* x, const float* W0, float* h, float* geo, int nw, int C,
+                  hipStream_t s);
+// Proposal (mcmc.py:67-102): x2 = sph_sampling(x, noise).
+void launch_propose(const Dims& d, const float* x, float* x2, int nw, float width, uint64_t seed, uint64_t step,
+                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s);
+void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t walker_offset, hipStream_t s);
+
+// attention.hip: channel self-attention for all heads.
+void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s);
+
+// layernorm.hip
+//   mode 0: h = LN_ch(X)           (X may alias h)
+//   mode 1: h = LN_ch(h + tanh_ch(Z))
+void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
+                      int nw, int C, int mode, hipStream_t s);
+
+// det.hip
+//   value mode (C == 1): logpsi[nw][2]
+//   energy mode (C == 2N+5): e_l[nw][2], obs[nw][8]
+void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
+                      float* logpsi, int nw, hipStream_t s);
+void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
+                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s);
+size_t det_energy_smem_bytes(const Dims& d);
+void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStream_t s);
+// mcmc.hip: accept/reject (mcmc.py:55-62).
+void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_acc,
+                   int nw, uint64_t seed, uint64_t step, int64_t walker_offset, const float* noise,
+                   int noise_stride, hipStream_t s);
+void launch_lp_from_logpsi(const float* logpsi, float* lp, int32_t* n_acc, int nw, hipStream_t s);
+
+// stats.hip
+void launch_stats(const float* e_l, const float* obs, const int32_t* n_acc, int B, int steps, float* out,
+                  float* scratch, hipStream_t s);
+
+}  // namespace dh

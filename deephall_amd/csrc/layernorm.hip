@@ -1,0 +1,210 @@
+// Channel LayerNorm (flax LayerNorm(epsilon=1e-5), psiformer.py:46,48), optionally
+// fused with the tanh MLP branch and its residual (psiformer.py:47):
+//
+//   mode 0:  h = LN_ch(X)
+//   mode 1:  h = LN_ch(h + tanh_ch(Z))
+//
+// One workgroup per (walker, electron); the [C][D] channel tile lives in LDS.
+// With z = x - mean_D(x) per channel, s = (mean(z0^2) + eps)^-1/2 and
+// a_c = s^2 mean(z0 z_c):
+//   n0   = s z0
+//   n_t  = s (z_t - a_t z0)
+//   n_L  = s (z_L - a_L z0 - 2 sum_t a_t z_t + z0 sum_t (3 a_t^2 - s^2 mean(z_t^2)))
+//   n_Sk = s (z_Sk - a_Sk z0 - 2 a_uk u_k + z0 (3 a_uk^2 - s^2 mean(u_k^2))),
+//          u_k = sum_t alpha_kt z_t,  a_uk = sum_t alpha_kt a_t
+//   y    = scale * n  (+ bias on the value channel)
+// tanh_ch: y0 = tanh z0, y_t = tanh' z_t, y_L = tanh' z_L + tanh'' sum_t z_t^2,
+//          y_Sk = tanh' z_Sk + tanh'' (sum_t alpha_kt z_t)^2.
+#include "dh_internal.h"
+#include "device_common.h"
+
+namespace dh {
+namespace {
+
+__global__ void layernorm_kernel(const float* X, const float* __restrict__ Z, const float* __restrict__ ln,
+                                 const float* __restrict__ geo, float* h, int N, int C, int D, int mode) {
+  extern __shared__ float sm[];
+  const int T = 2 * N;
+  const bool ch = C > 1;
+  float* tile = sm;                       // [C][D]
+  float* u = tile + (size_t)C * D;        // [3][D]       (ch only)
+  float* al = u + (ch ? 3 * D : 0);       // [3][T]
+  float* red = al + (ch ? 3 * T : 0);     // reductions: mu[C], p[C], q[T], uu[3]
+  float* coef = red + 2 * C + T + 4;      // s, coefL, au[3], coefS[3]
+  const int e = blockIdx.x;               // walker*N + electron
+  const int b = e / N;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wid = tid >> 6, nwav = nt >> 6;
+  const size_t row0 = (size_t)e * C;
+
+  if (ch) {
+    for (int t = tid; t < T; t += nt) {
+      const int i = t >> 1;
+      const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+      for (int k = 0; k < 3; ++k) {
+        float a;
+        if ((t & 1) == 0)
+          a = (k == 0) ? -g.z : (k == 1 ? g.w : 0.f);
+        else
+          a = (k == 0) ? -(g.y * g.w) : (k == 1 ? -(g.y * g.z) : g.x);
+        al[k * T + t] = a;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- load (and optionally apply residual + tanh channel rule)
+  for (int d = tid; d < D; d += nt) {
+    if (mode == 0) {
+      for (int c = 0; c < C; ++c) tile[c * D + d] = X[(row0 + c) * D + d];
+    } else {
+      const float z0 = Z[row0 * D + d];
+      const float y0 = tanhf(z0);
+      const float d1 = 1.f - y0 * y0;
+      const float d2 = -2.f * y0 * d1;
+      tile[d] = h[row0 * D + d] + y0;
+      if (ch) {
+        float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+        for (int t = 0; t < T; ++t) {
+          const float zt = Z[(row0 + 1 + t) * D + d];
+          sq = fmaf(zt, zt, sq);
+          u0 = fmaf(al[t], zt, u0);
+          u1 = fmaf(al[T + t], zt, u1);
+          u2 = fmaf(al[2 * T + t], zt, u2);
+          tile[(1 + t) * D + d] = h[(row0 + 1 + t) * D + d] + d1 * zt;
+        }
+        const float zl = Z[(row0 + 1 + T) * D + d];
+        tile[(1 + T) * D + d] = h[(row0 + 1 + T) * D + d] + d1 * zl + d2 * sq;
+        const float uu[3] = {u0, u1, u2};
+        for (int k = 0; k < 3; ++k) {
+          const int c = 2 + T + k;
+          const float zs = Z[(row0 + c) * D + d];
+          tile[c * D + d] = h[(row0 + c) * D + d] + d1 * zs + d2 * uu[k] * uu[k];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- channel means
+  float* mu = red;
+  for (int c = wid; c < C; c += nwav) {
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) s += tile[c * D + d];
+    s = wave_sum(s);
+    if (lane == 0) mu[c] = s / D;
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += nt) {
+    for (int c = 0; c < C; ++c) tile[c * D + d] -= mu[c];
+    if (ch) {
+      float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+      for (int t = 0; t < T; ++t) {
+        const float zt = tile[(1 + t) * D + d];
+        u0 = fmaf(al[t], zt, u0);
+        u1 = fmaf(al[T + t], zt, u1);
+        u2 = fmaf(al[2 * T + t], zt, u2);
+      }
+      u[d] = u0;
+      u[D + d] = u1;
+      u[2 * D + d] = u2;
+    }
+  }
+  __syncthreads();
+
+  // ---- reductions: p_c = mean(z0 z_c), q_t = mean(z_t^2), uu_k = mean(u_k^2)
+  float* p = red + C;
+  float* q = p + C;
+  float* uu = q + T;
+  const int nred = ch ? (C + T + 3) : 1;
+  for (int r = wid; r < nred; r += nwav) {
+    float s = 0.f;
+    if (r < C) {
+      for (int d = lane; d < D; d += 64) s = fmaf(tile[d], tile[r * D + d], s);
+    } else if (r < C + T) {
+      const int t = r - C;
+      for (int d = lane; d < D; d += 64) {
+        const float v = tile[(1 + t) * D + d];
+        s = fmaf(v, v, s);
+      }
+    } else {
+      const int k = r - C - T;
+      for (int d = lane; d < D; d += 64) {
+        const float v = u[k * D + d];
+        s = fmaf(v, v, s);
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+      if (r < C)
+        p[r] = s / D;
+      else if (r < C + T)
+        q[r - C] = s / D;
+      else
+        uu[r - C - T] = s / D;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float s = 1.f / sqrtf(p[0] + 1e-5f);
+    coef[0] = s;
+    if (ch) {
+      const float s2 = s * s;
+      float cl = 0.f;
+      for (int t = 0; t < T; ++t) {
+        const float at = s2 * p[1 + t];
+        cl += 3.f * at * at - s2 * q[t];
+      }
+      coef[1] = cl;
+      for (int k = 0; k < 3; ++k) {
+        float au = 0.f;
+        for (int t = 0; t < T; ++t) au = fmaf(al[k * T + t], s2 * p[1 + t], au);
+        coef[2 + k] = au;
+        coef[5 + k] = 3.f * au * au - s2 * uu[k];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- outputs
+  const float s = coef[0];
+  const float* gam = ln;
+  const float* bet = ln + D;
+  for (int d = tid; d < D; d += nt) {
+    const float g = gam[d];
+    const float z0 = tile[d];
+    h[row0 * D + d] = g * (s * z0) + bet[d];
+    if (ch) {
+      const float s2 = s * s;
+      float sum_at_zt = 0.f;
+      for (int t = 0; t < T; ++t) {
+        const float at = s2 * p[1 + t];
+        const float zt = tile[(1 + t) * D + d];
+        sum_at_zt = fmaf(at, zt, sum_at_zt);
+        h[(row0 + 1 + t) * D + d] = g * s * (zt - at * z0);
+      }
+      const float aL = s2 * p[1 + T];
+      const float nL = tile[(1 + T) * D + d] - aL * z0 - 2.f * sum_at_zt + coef[1] * z0;
+      h[(row0 + 1 + T) * D + d] = g * s * nL;
+      for (int k = 0; k < 3; ++k) {
+        const int c = 2 + T + k;
+        const float aS = s2 * p[c];
+        const float nS = tile[c * D + d] - aS * z0 - 2.f * coef[2 + k] * u[k * D + d] + coef[5 + k] * z0;
+        h[(row0 + c) * D + d] = g * s * nS;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
+                      int nw, int C, int mode, hipStream_t s) {
+  const bool ch = C > 1;
+  const size_t floats = (size_t)C * d.D + (ch ? 3 * d.D + 3 * d.T : 0) + 2 * C + d.T + 4 + 8;
+  const int threads = 256;
+  ensure_smem(layernorm_kernel, floats * sizeof(float));
+  hipLaunchKernelGGL(layernorm_kernel, dim3(nw * d.N), dim3(threads), floats * sizeof(float), s, X, Z, ln, geo, h,
+                     d.N, C, d.D, mode);
+}
+
+}  // namespace dh

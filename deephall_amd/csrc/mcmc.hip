@@ -1,0 +1,123 @@
+// Metropolis-Hastings pieces of the walker update (deephall/mcmc.py).
+//
+//   propose_kernel  sph_sampling (mcmc.py:67-102): theta' = arctan(xi * width),
+//                   phi' = 2 pi U, rotate the pole onto each electron with
+//                   R_z(phi) R_y(theta), back to (theta, phi) with clipping.
+//   accept_kernel   mh_update accept/select (mcmc.py:55-62): accept the whole
+//                   walker if 2 Re log psi(x') - lp > log U.
+//   init_kernel     init_guess (train.py:40-54): theta = arccos U(-1,1), phi = U(-pi,pi).
+//
+// Random numbers: Philox4x32-10 keyed by the seed, counter (lane, global walker,
+// step) — see device_common.h — or injected arrays [B][2N+1] per step
+// (normals[N], phi uniforms[N], accept uniform) for parity tests.
+#include "dh_internal.h"
+#include "device_common.h"
+
+namespace dh {
+namespace {
+
+constexpr int kPurposeMcmc = 0, kPurposeInit = 1;
+
+__global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ x2, int nw, int N, float width,
+                               uint64_t seed, uint64_t step, int64_t woff, const float* __restrict__ noise) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nw * N) return;
+  const int b = e / N, i = e % N;
+  float xi, up;
+  if (noise) {
+    xi = noise[(size_t)b * (2 * N + 1) + i];
+    up = noise[(size_t)b * (2 * N + 1) + N + i];
+  } else {
+    u32x4 r = dh_random(seed, kPurposeMcmc, (uint32_t)i, (uint64_t)(woff + b), step);
+    xi = box_muller(r.x, r.y);
+    up = u01(r.z);
+  }
+  const float th = x[2 * e], ph = x[2 * e + 1];
+  const float thp = atanf(xi * width);
+  const float php = up * 2.f * kPi;
+  float stp, ctp, spp, cpp, st, ct, sp, cp;
+  sincosf(thp, &stp, &ctp);
+  sincosf(php, &spp, &cpp);
+  sincosf(th, &st, &ct);
+  sincosf(ph, &sp, &cp);
+  const float X = stp * cpp, Y = stp * spp, Z = ctp;
+  // R_y(theta) then R_z(phi)
+  const float ax = ct * X + st * Z, ay = Y, az = -st * X + ct * Z;
+  const float x2x = cp * ax - sp * ay, x2y = sp * ax + cp * ay, x2z = az;
+  const float thn = acosf(fminf(fmaxf(x2z, -1.f), 1.f));
+  const float sgn = (x2y > 0.f) ? 1.f : ((x2y < 0.f) ? -1.f : 0.f);
+  const float q = x2x / sinf(thn);
+  // clip(q) with NaN propagation as jnp.clip (NaN in -> NaN out)
+  const float qc = (q != q) ? q : fminf(fmaxf(q, -1.f), 1.f);
+  const float phn = sgn * acosf(qc);
+  x2[2 * e] = thn;
+  x2[2 * e + 1] = phn;
+}
+
+__global__ void accept_kernel(float* __restrict__ x, const float* __restrict__ x2, float* __restrict__ lp,
+                              const float* __restrict__ logpsi2, int32_t* __restrict__ nacc, int nw, int N,
+                              uint64_t seed, uint64_t step, int64_t woff, const float* __restrict__ noise) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nw) return;
+  float u;
+  if (noise) {
+    u = noise[(size_t)b * (2 * N + 1) + 2 * N];
+  } else {
+    u32x4 r = dh_random(seed, kPurposeMcmc, (uint32_t)N, (uint64_t)(woff + b), step);
+    u = u01(r.x);
+  }
+  const float lp2 = 2.f * logpsi2[2 * b];
+  const bool cond = (lp2 - lp[b]) > logf(u);
+  if (cond) {
+    for (int k = 0; k < 2 * N; ++k) x[(size_t)b * 2 * N + k] = x2[(size_t)b * 2 * N + k];
+    lp[b] = lp2;
+    nacc[b] += 1;
+  }
+}
+
+__global__ void lp_init_kernel(const float* __restrict__ logpsi, float* __restrict__ lp, int32_t* __restrict__ nacc,
+                               int nw) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nw) return;
+  lp[b] = 2.f * logpsi[2 * b];
+  nacc[b] = 0;
+}
+
+__global__ void init_kernel(float* __restrict__ x, int nw, int N, uint64_t seed, int64_t woff) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nw * N) return;
+  const int b = e / N, i = e % N;
+  u32x4 r = dh_random(seed, kPurposeInit, (uint32_t)i, (uint64_t)(woff + b), 0);
+  const float u1 = u01(r.x), u2 = u01(r.y);
+  x[2 * e] = acosf(2.f * u1 - 1.f);
+  x[2 * e + 1] = (2.f * u2 - 1.f) * kPi;
+}
+
+}  // namespace
+
+void launch_propose(const Dims& d, const float* x, float* x2, int nw, float width, uint64_t seed, uint64_t step,
+                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s) {
+  (void)noise_stride;
+  const int n = nw * d.N;
+  hipLaunchKernelGGL(propose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, x2, nw, d.N, width, seed, step,
+                     walker_offset, noise);
+}
+
+void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_acc,
+                   int nw, uint64_t seed, uint64_t step, int64_t walker_offset, const float* noise,
+                   int noise_stride, hipStream_t s) {
+  (void)noise_stride;
+  hipLaunchKernelGGL(accept_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, x, x2, lp, logpsi2, n_acc, nw, d.N,
+                     seed, step, walker_offset, noise);
+}
+
+void launch_lp_from_logpsi(const float* logpsi, float* lp, int32_t* n_acc, int nw, hipStream_t s) {
+  hipLaunchKernelGGL(lp_init_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, logpsi, lp, n_acc, nw);
+}
+
+void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t walker_offset, hipStream_t s) {
+  const int n = nw * d.N;
+  hipLaunchKernelGGL(init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, nw, d.N, seed, walker_offset);
+}
+
+}  // namespace dh

@@ -1,0 +1,116 @@
+"""VMC inner loop driver — the hot-path callers of deephall/train.py.
+
+Reproduces, for the inference step (``optim.optimizer=none``,
+optimizers/none.py:22-35), the reference's setup and loop ordering:
+
+* ``init_guess`` (train.py:40-54) — uniform walkers on the sphere, device RNG
+* ``initalize_state`` (train.py:57-65) — walkers sharded contiguously by rank
+* ``setup_mcmc`` (train.py:68-77)
+* ``vmc`` — burn-in (train.py:107-111), then per iteration: mcmc_step
+  (128-130), update_mcmc_width (131-137), energy statistics (140), log
+  (141-152), NaN abort (159-167).  One packed all-reduce per iteration.
+
+Multi-GPU: one process per GPU (torchrun-style env); each rank owns
+batch_size / world_size walkers.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib, constants
+from .config import Config
+from .loss import device_stats, reduce_stats
+from .hamiltonian import _run_local_energy
+from .mcmc import make_mcmc_step, update_mcmc_width
+from .networks import make_network
+from .networks.psiformer import _ptr, _stream, get_handle
+from .random import Key, PRNGKey
+
+logger = logging.getLogger("deephall_amd")
+
+
+def init_distributed(backend: str | None = None):
+    """Initialise torch.distributed from torchrun env vars if WORLD_SIZE > 1."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1 and not dist.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return constants.rank(), constants.world_size()
+
+
+def init_guess(key: Key, batch: int, nelec: int, device=None, walker_offset: int = 0, network=None) -> torch.Tensor:
+    """train.py:40-54 on the device: theta = arccos U(-1,1), phi = U(-pi,pi)."""
+    device = torch.device(device or "cuda")
+    if network is None:
+        from .networks.psiformer import NetworkSpec
+
+        spec = NetworkSpec(nspins=(nelec, 0), flux=2, ndets=1, num_heads=1, heads_dim=4, num_layers=0)
+    else:
+        spec = network.spec
+    h = get_handle(spec, device)
+    x = torch.empty(batch, nelec, 2, dtype=torch.float32, device=device)
+    _lib.check(h.lib.dh_init_walkers(h.h, _ptr(x), batch, int(key.seed), int(walker_offset), _stream(device)))
+    return x
+
+
+def initalize_state(cfg: Config, model, device=None):
+    """train.py:57-65: returns (step, (params, data, opt_state, mcmc_width)) for this rank."""
+    r, n = constants.rank(), constants.world_size()
+    if cfg.batch_size % n:
+        raise ValueError("batch_size must be divisible by the number of GPUs")
+    per = cfg.batch_size // n
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    data = init_guess(Key(cfg.seed * 2 + 1), per, sum(cfg.system.nspins), device, walker_offset=r * per, network=model)
+    params = model.init(PRNGKey(cfg.seed), data, device=device)
+    return 0, (params, data, None, float(cfg.mcmc.width))
+
+
+def setup_mcmc(cfg: Config, model):
+    """train.py:68-77."""
+    per = cfg.batch_size // constants.world_size()
+    step = make_mcmc_step(model, batch_per_device=per, steps=cfg.mcmc.steps)
+    pmoves = np.zeros(cfg.mcmc.adapt_frequency)
+    return step, pmoves
+
+
+def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | None = None):
+    """Inference-mode VMC loop (optimizer 'none').  Returns the list of per-iteration stats."""
+    init_distributed()
+    model = make_network(cfg.system, cfg.network)
+    _, (params, data, _, width) = initalize_state(cfg, model)
+    mcmc_step, pmoves = setup_mcmc(cfg, model)
+    key = PRNGKey(cfg.seed)
+    steps = cfg.mcmc.steps
+    for _ in range(cfg.mcmc.burn_in if burn_in is None else burn_in):
+        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        key = key.advance(steps)
+    history = []
+    iters = cfg.optim.iterations if iterations is None else iterations
+    for t in range(iters):
+        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        key = key.advance(steps)
+        e_l, obs = _run_local_energy(model, params, data)
+        local = device_stats(model, e_l, obs, mcmc_step.last_n_accept, steps)
+        stats = reduce_stats(local)  # the single all-reduce of this iteration
+        width, pmoves = update_mcmc_width(t, width, cfg.mcmc.adapt_frequency, stats["pmove"], pmoves)
+        row = {k: (complex(v.item()) if v.is_complex() else float(v.item())) for k, v in stats.items()}
+        history.append(row)
+        if log is not None and constants.rank() == 0:
+            log(
+                f"step={t} pmove={row['pmove']:.2f} energy={row['energy'].real:.4f} "
+                f"energy_imag={row['energy'].imag:+.4f} variance={row['variance']:.4f} "
+                f"Lz={row['angular_momentum_z']:+.4f} L_square={row['angular_momentum_square']:.4f}"
+            )
+        if np.isnan(row["energy"].real):
+            raise SystemExit("=" * 30 + " ABORT " + "=" * 30)
+    return history

@@ -1,0 +1,171 @@
+/*
+ * deephall_amd.h — C ABI of the MI355X-native DeepHall VMC inner loop.
+ *
+ * The reference (peterzjx/DeepHall) has no FFI: its hot path is a set of Python
+ * callables transformed by JAX.  This ABI is the native drop-in underneath the
+ * Python mirror of those callables (deephall_amd/), one entry point per
+ * reference interface:
+ *
+ *   dh_create / dh_set_params   <-> make_network(system, network)
+ *                                   deephall/networks/__init__.py:22-37, and the
+ *                                   parameter tree of model.init (train.py:62)
+ *   dh_logpsi                   <-> Psiformer.__call__ / model.apply, vmapped
+ *                                   deephall/networks/psiformer.py:72-76, train.py:69,84
+ *   dh_mcmc_step                <-> make_mcmc_step(...)(params, data, key, width)
+ *                                   deephall/mcmc.py:105-150 (mh_update 25-64,
+ *                                   sph_sampling 67-102)
+ *   dh_local_energy             <-> local_energy(f, system) vmapped
+ *                                   deephall/hamiltonian.py:175-212 (+ make_local_kinetic_energy 83-172,
+ *                                   make_potential 63-80), loss.py:51
+ *   dh_energy_stats             <-> device-local statistics of loss_and_grad
+ *                                   deephall/loss.py:30-38, 66-92 (before pmean)
+ *   dh_init_walkers             <-> init_guess, deephall/train.py:40-54
+ *
+ * Conventions
+ *   - Every pointer argument except `cfg`/`out`/`offsets` is a DEVICE pointer.
+ *     Buffers (including the workspace) are owned by the caller; the library
+ *     owns only the handle and the packed parameter copy made by dh_set_params.
+ *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = default stream).
+ *     One handle per device; a handle is not thread-safe.
+ *   - Return 0 on success, a negative DH_E* code on error; dh_last_error()
+ *     returns a thread-local message.  No C++ exception crosses the ABI.
+ *     NaN walkers propagate as NaN exactly as in the reference (loss.py uses
+ *     nanmean; train.py:159 aborts on a NaN energy).
+ *   - Walker coordinates: float32 [B][N][2] = (theta, phi), as the reference's
+ *     data[B, N, 2] (train.py:53).
+ */
+#ifndef DEEPHALL_AMD_H
+#define DEEPHALL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DH_OK 0
+#define DH_EINVAL -1   /* bad argument / shape / unsupported config */
+#define DH_EHIP -2     /* HIP runtime error */
+#define DH_ENOMEM -3   /* workspace too small */
+#define DH_ESTATE -4   /* parameters not set */
+
+#define DH_INTERACTION_COULOMB 0
+#define DH_INTERACTION_HARMONIC 1
+#define DH_ORBITAL_FULL 0
+#define DH_ORBITAL_SPARSE 1 /* not supported yet: dh_create returns DH_EINVAL */
+
+/* System + Network fields of deephall/config.py:56-104 that the hot path reads. */
+typedef struct dh_config {
+  int n_up, n_dn;             /* System.nspins                          */
+  int flux;                   /* System.flux = 2Q                       */
+  float radius;               /* System.radius; <= 0 means sqrt(Q)      */
+  float interaction_strength; /* System.interaction_strength            */
+  int interaction_type;       /* DH_INTERACTION_*                       */
+  int num_heads;              /* PsiformerNetwork.num_heads             */
+  int heads_dim;              /* PsiformerNetwork.heads_dim             */
+  int num_layers;             /* PsiformerNetwork.num_layers            */
+  int ndets;                  /* PsiformerNetwork.determinants          */
+  int orbital_type;           /* Network.orbital, DH_ORBITAL_*          */
+} dh_config;
+
+typedef struct dh_handle dh_handle;
+
+int dh_create(const dh_config* cfg, dh_handle** out);
+void dh_destroy(dh_handle* h);
+const char* dh_last_error(void);
+const char* dh_version(void);
+
+/* Packed parameter layout.  Segment s starts at float offset
+ * offsets[s] of the packed buffer (each segment 64-float aligned); segment
+ * order:
+ *   0                  W0        [4][D]           PsiformerLayers_0/Dense_0/kernel
+ *   per layer l (8 segments, base 1+8l):
+ *     +0 Wqkv [D][3D]  query|key|value kernels, columns (h, d) per block
+ *     +1 bqkv [3D]
+ *     +2 Wol  [D][D]   out/kernel (as [H*dh][D]) @ Dense_{2l+1}/kernel  (folded)
+ *     +3 bol  [D]      out/bias @ Dense_{2l+1}/kernel
+ *     +4 ln1  [2][D]   LayerNorm_{2l}: scale, bias
+ *     +5 Wm   [D][D]   Dense_{2l+2}/kernel
+ *     +6 bm   [D]      Dense_{2l+2}/bias
+ *     +7 ln2  [2][D]   LayerNorm_{2l+1}: scale, bias
+ *   1+8L     Worb [D][ld_orb]  columns ((blk*2+part)*M + m)*N*K + j*K + k,
+ *                              blk = spin block, part 0 = real / 1 = imag,
+ *                              zero padded to ld_orb (multiple of 128)
+ *   2+8L     borb [ld_orb]
+ *   3+8L     jastrow [2]       ee_par, ee_anti
+ * Returns the number of segments (3+8L) and writes up to `n` offsets; the
+ * total float count is offsets[nseg] (written if n > nseg). */
+int dh_param_layout(const dh_handle* h, size_t* offsets, int n);
+/* Copy the packed parameter buffer (device pointer, `count` floats) into the
+ * handle.  `count` must equal the total from dh_param_layout. */
+int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream);
+
+/* Workspace bytes needed to process `batch` walkers: op 0 = log psi / MCMC,
+ * op 1 = local energy.  Local energy processes walkers in chunks sized to the
+ * workspace it is given (at least one walker). */
+size_t dh_workspace_bytes(const dh_handle* h, int batch, int op);
+
+/* log psi for B walkers: logpsi[B][2] = (Re, Im), Im the principal phase. */
+int dh_logpsi(dh_handle* h, const float* x, int B, float* logpsi, void* ws, size_t ws_bytes, void* stream);
+
+/* `steps` Metropolis-Hastings all-electron moves on B walkers, in place.
+ *   x       [B][N][2]  walkers, updated in place (the reference donates data)
+ *   lp      [B]        work/out: 2 Re log psi of the current walkers (computed
+ *                      here at entry, mcmc.py:142)
+ *   n_accept[B] int32  out: accepted moves per walker in this call
+ *   width              proposal width (MCMC.width, mcmc.py:69-70)
+ *   seed, counter      counter-based RNG (Philox4x32-10): the draw for walker g
+ *                      (global index = walker_offset + b), step s uses counter
+ *                      (g, counter + s, electron, 0) under key seed; results do
+ *                      not depend on how walkers are sharded over devices
+ *   noise              NULL, or injected noise [steps][B][2N+1] floats:
+ *                      normals [N], phi uniforms in [0,1) [N], accept uniform [1]
+ */
+int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, int steps, float width,
+                 uint64_t seed, uint64_t counter, int64_t walker_offset, const float* noise, void* ws,
+                 size_t ws_bytes, void* stream);
+
+/* Local energy for B walkers.
+ *   e_l [B][2]   E_L = KE + lambda * PE (complex)
+ *   obs [B][8]   KE re, KE im, PE (already times interaction_strength),
+ *                Lz, Lz^2, L^2, logpsi re, logpsi im                         */
+int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs, void* ws, size_t ws_bytes,
+                    void* stream);
+
+/* Device-local energy statistics (loss.py:66-92 before the pmean).  Writes
+ * out[DH_NSTATS] floats: see DH_STAT_* indices.  B <= 32768.  */
+#define DH_NSTATS 16
+#define DH_STAT_ENERGY_RE 0    /* nanmean Re E_L                     */
+#define DH_STAT_ENERGY_IM 1    /* nanmean Im E_L                     */
+#define DH_STAT_CLIPPED_RE 2   /* nanmean Re iqr_clip(E_L)           */
+#define DH_STAT_CLIPPED_IM 3   /* nanmean Im iqr_clip(E_L)           */
+#define DH_STAT_ERE2 4         /* nanmean (Re E_L)^2                 */
+#define DH_STAT_KINETIC_RE 5   /* mean KE re                         */
+#define DH_STAT_KINETIC_IM 6   /* mean KE im                         */
+#define DH_STAT_POTENTIAL 7    /* mean PE                            */
+#define DH_STAT_LZ 8           /* mean Lz                            */
+#define DH_STAT_LZ2 9          /* mean Lz^2                          */
+#define DH_STAT_L2 10          /* mean L^2                           */
+#define DH_STAT_PMOVE 11       /* sum n_accept / (steps * B)         */
+#define DH_STAT_NVALID 12      /* number of non-NaN E_L              */
+int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int32_t* n_accept, int B, int steps,
+                    float* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Potential energy only (make_potential, hamiltonian.py:63-80), NOT multiplied by
+ * interaction_strength: pe[B]. */
+int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream);
+
+/* Test hooks: run the network trunk + orbital GEMM only and leave the
+ * activations in the workspace (trunk output at float offset 0, orbital
+ * features at float offset dh_debug_f_offset). */
+int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t ws_bytes, void* stream);
+size_t dh_debug_f_offset(const dh_handle* h, int B, int op);
+
+/* init_guess with the device RNG: theta = arccos U(-1,1), phi = U(-pi,pi). */
+int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEEPHALL_AMD_H */

@@ -1,0 +1,57 @@
+"""Shared test helpers: configs, deterministic params/walkers, oracle bridges."""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from oracle import reference as R
+
+# BASELINE.json configs used for parity (C1 .. C5); B is the test batch, not the bench batch.
+CONFIGS = {
+    "C1": dict(nspins=(3, 0), flux=2),
+    "C2": dict(nspins=(6, 0), flux=15),
+    "C4": dict(nspins=(10, 0), flux=23),
+    "C5": dict(nspins=(20, 0), flux=57),
+    "MIX": dict(nspins=(2, 2), flux=5, num_heads=2, heads_dim=8, determinants=2),
+}
+
+
+def oracle_config(name, **over):
+    kw = dict(CONFIGS[name])
+    kw.update(over)
+    return R.OracleConfig(**kw)
+
+
+def make_params(cfg: R.OracleConfig, seed=42, perturb=True):
+    """float32-representable params (so GPU and oracle see identical weights)."""
+    p = R.init_params(cfg, seed=seed)
+    if perturb:
+        g = np.random.default_rng(seed + 1)
+        for k in sorted(p):
+            if k.endswith("bias") or k.endswith("scale"):
+                p[k] = p[k] + torch.tensor(0.1 * g.standard_normal(p[k].shape))
+        p["Jastrow_0/ee_par"][:] = 0.7
+        p["Jastrow_0/ee_anti"][:] = 1.3
+    return {k: v.float().double() for k, v in p.items()}
+
+
+def make_walkers(B, N, seed=1898, margin=0.15):
+    """float32 walkers drawn like init_guess, kept `margin` rad away from the poles
+    (f32 E_L loses digits as sin(theta) -> 0 in the reference too)."""
+    g = np.random.default_rng(seed)
+    x = R.init_guess_from_uniforms(g.random((B, N)), g.random((B, N)))
+    x[..., 0] = np.clip(x[..., 0], margin, math.pi - margin)
+    return x.astype(np.float32)
+
+
+def to_device_params(p):
+    return {k: v.float().cuda() for k, v in p.items()}
+
+
+def rel_err(a, b, floor=1.0):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), floor)))
