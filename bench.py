@@ -1,0 +1,226 @@
+"""Benchmark: the DeepHall VMC inner loop on MI355X (BASELINE.json metric).
+
+One "step" = one VMC iteration of the reference's loop body (train.py:126-140)
+without the optimizer: ``mcmc_step`` (10 all-electron Metropolis moves = 11
+log-psi evaluations per walker, mcmc.py:122-148) + the local energy of every
+walker (hamiltonian.py:175-212) + the device statistics and ONE packed
+all-reduce (loss.py:66-92).  Workload: BASELINE.json configs[1] — nspins=[6,0],
+flux=15, default Psiformer (4 heads x 64, 2 layers, 1 determinant), 4096
+walkers per GPU, random-init weights, walkers from init_guess + burn-in.
+
+value = local energies per second over all GPUs (= walkers x GPUs / step time);
+walker_steps_per_sec = 10 x that.  Multi-GPU: weak scaling, walkers sharded,
+one all-reduce of 12 floats per step.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "local-energies/sec + MCMC walker-steps/sec, N=6 2Q=15, 1/2/4/8 GPUs"
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="walkers per GPU")
+    ap.add_argument("--nspins", type=int, nargs=2, default=[6, 0])
+    ap.add_argument("--flux", type=int, default=15)
+    ap.add_argument("--mcmc-steps", type=int, default=10)
+    ap.add_argument("--burn-in", type=int, default=5)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+
+    from deephall_amd import _lib, config
+    from deephall_amd.hamiltonian import _run_local_energy
+    from deephall_amd.loss import device_stats, reduce_stats
+    from deephall_amd.mcmc import make_mcmc_step
+    from deephall_amd.networks import make_network
+    from deephall_amd.networks.psiformer import get_handle
+    from deephall_amd.random import Key, PRNGKey
+    from deephall_amd.train import init_guess
+
+    lib = _lib.load()
+    system = config.System(nspins=tuple(args.nspins), flux=args.flux)
+    model = make_network(system, config.Network())
+    B = args.batch
+    N = sum(args.nspins)
+    params = model.init(PRNGKey(42), device=dev)
+    data = init_guess(Key(4242), B, N, dev, walker_offset=rank * B, network=model)
+    steps = args.mcmc_steps
+    mcmc_step = make_mcmc_step(model, batch_per_device=B, steps=steps)
+    key = PRNGKey(7)
+    width = 0.1
+
+    def vmc_step(data, key):
+        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        e_l, obs = _run_local_energy(model, params, data)
+        local_stats = device_stats(model, e_l, obs, mcmc_step.last_n_accept, steps)
+        stats = reduce_stats(local_stats)  # the one all-reduce of the step
+        return data, stats
+
+    for _ in range(args.burn_in):
+        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        key = key.advance(steps)
+    for _ in range(args.warmup):
+        data, stats = vmc_step(data, key)
+        key = key.advance(steps)
+    h = get_handle(model.spec, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    # ---------------- timed region (kernel events recorded live for the roofline)
+    lib.dh_profile_enable(h.h, 1)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        data, stats = vmc_step(data, key)
+        key = key.advance(steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    import ctypes as C
+
+    prof = (C.c_double * (4 * 7))()
+    lib.dh_profile_read(h.h, prof, 1)
+    lib.dh_profile_enable(h.h, 0)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    energy = complex(stats["energy"].item())
+    pmove = float(stats["pmove"].item())
+
+    # ---------------- component rates (untimed for `value`): MCMC-only and E_L-only
+    barrier()
+    a = time.perf_counter()
+    for _ in range(3):
+        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        key = key.advance(steps)
+    barrier()
+    t_mcmc = (time.perf_counter() - a) / 3
+    a = time.perf_counter()
+    for _ in range(3):
+        _run_local_energy(model, params, data)
+    barrier()
+    t_el = (time.perf_counter() - a) / 3
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    kinds = _lib.PROF_KINDS
+    kern = {}
+    for i, k in enumerate(kinds):
+        cnt, ms, fl, by = prof[4 * i : 4 * i + 4]
+        if cnt:
+            kern[k] = {
+                "launches_per_step": cnt / args.steps,
+                "ms_per_step": ms / args.steps,
+                "avg_us": 1e3 * ms / cnt,
+            }
+    g_cnt, g_ms, g_fl, g_by = prof[0:4]
+    achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
+    roofline = {
+        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)",
+        "bound": "mfma",
+        "achieved": round(achieved, 2),
+        "peak": PEAK_F32_MFMA_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+        "traffic": None,
+        "flops_per_launch": g_fl / g_cnt if g_cnt else 0,
+        "avg_launch_us": 1e3 * g_ms / g_cnt if g_cnt else 0,
+        "gemm_share_of_step": round(g_ms / (dt * 1e3), 4) if dt else None,
+    }
+    B_total = B * world
+    value = B_total * args.steps / dt
+    F_fwd = 2 * N * 4 * 256 + 2 * (12 * N * 256**2 + 4 * N * N * 256) + 4 * N * 256 * (args.flux + 1) * N
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "local-energies/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (init_guess walkers + burn-in, random-init Psiformer weights)",
+        "config": {
+            "workload": f"VMC iteration (mcmc_step {steps} MH moves + local energy + stats all-reduce), "
+            f"nspins={list(args.nspins)} flux={args.flux}, Psiformer 4x64 heads, 2 layers, 1 det",
+            "walkers_per_gpu": B,
+            "global_batch": B_total,
+            "parallelism": f"walker-dp{world}",
+        },
+        "walker_steps_per_sec": round(value * steps, 1),
+        "components": {
+            "mcmc_step_ms": round(1e3 * t_mcmc, 3),
+            "local_energy_ms": round(1e3 * t_el, 3),
+            "walker_steps_per_sec_mcmc_only": round(B_total * steps / t_mcmc, 1),
+            "local_energies_per_sec_el_only": round(B_total / t_el, 1),
+            "model_tflops_el_only": round(B_total * (2 * N + 5) * F_fwd / t_el / 1e12, 2),
+            "model_tflops_mcmc_only": round(B_total * (steps + 1) * F_fwd / t_mcmc / 1e12, 2),
+        },
+        "kernels": kern,
+        "roofline": roofline,
+        "energy": [round(energy.real, 5), round(energy.imag, 5)],
+        "pmove": round(pmove, 3),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+        from oracle.reference import OracleConfig
+
+        threads = min(16, os.cpu_count() or 1)
+        cb = cpu_baseline.measure(
+            OracleConfig(nspins=tuple(args.nspins), flux=args.flux), steps=steps,
+            budget_s=args.cpu_baseline_seconds, threads=threads,
+        )
+        out["cpu_baseline"] = {
+            "value": round(cb["local_energies_per_sec"], 3),
+            "unit": "local-energies/s",
+            "cores": cb["threads"],
+            "kind": "port",
+            "sample": cb["sample"],
+            "walker_steps_per_sec": round(cb["walker_steps_per_sec"] * steps / (steps + 1), 1),
+            "el_only_per_sec": round(cb["el_only_per_sec"], 3),
+        }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

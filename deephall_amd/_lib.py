@@ -43,8 +43,13 @@ EXPORTS = [
     "dh_init_walkers",
     "dh_potential",
     "dh_debug_trunk",
+    "dh_profile_enable",
+    "dh_profile_read",
     "dh_debug_f_offset",
 ]
+
+
+PROF_KINDS = ["gemm", "attention", "layernorm", "input", "det_value", "det_energy", "mcmc"]
 
 
 class DhConfig(C.Structure):
@@ -107,6 +112,10 @@ def load(path: Path | str | None = None):
     lib.dh_debug_trunk.restype = i32
     lib.dh_debug_f_offset.argtypes = [vp, i32, i32]
     lib.dh_debug_f_offset.restype = sz
+    lib.dh_profile_enable.argtypes = [vp, i32]
+    lib.dh_profile_enable.restype = i32
+    lib.dh_profile_read.argtypes = [vp, C.POINTER(C.c_double), i32]
+    lib.dh_profile_read.restype = i32
     _lib = lib
     return lib
 

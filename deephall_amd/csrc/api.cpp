@@ -74,6 +74,19 @@ Work carve(const Dims& d, int nw, int C, void* base) {
 
 }  // namespace
 
+// Optional per-kernel HIP-event timing (bench.py reads it to compute the live roofline).
+enum ProfKind { PK_GEMM = 0, PK_ATTN, PK_LN, PK_INPUT, PK_DET_VALUE, PK_DET_ENERGY, PK_MCMC, PK_COUNT };
+struct ProfRec {
+  hipEvent_t a, b;
+  int kind;
+  double flops, bytes;
+};
+struct Profiler {
+  bool on = false;
+  std::vector<ProfRec> recs;
+  size_t used = 0;
+};
+
 struct dh_handle {
   dh_config cfg;
   Dims d;
@@ -83,7 +96,35 @@ struct dh_handle {
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
   std::vector<float> norm_host;
   bool params_set = false;
+  Profiler prof;
 };
+
+namespace {
+struct ProfScope {
+  dh_handle* h;
+  hipStream_t s;
+  ProfRec* r = nullptr;
+  ProfScope(dh_handle* h_, int kind, double flops, double bytes, hipStream_t s_) : h(h_), s(s_) {
+    if (!h->prof.on) return;
+    Profiler& P = h->prof;
+    if (P.used == P.recs.size()) {
+      ProfRec nr{};
+      (void)hipEventCreate(&nr.a);
+      (void)hipEventCreate(&nr.b);
+      P.recs.push_back(nr);
+    }
+    r = &P.recs[P.used++];
+    r->kind = kind;
+    r->flops = flops;
+    r->bytes = bytes;
+    (void)hipEventRecord(r->a, s);
+  }
+  ~ProfScope() {
+    if (r) (void)hipEventRecord(r->b, s);
+  }
+};
+}  // namespace
+#define PROF(kind, flops, bytes) ProfScope prof_scope_##__LINE__(h, kind, (double)(flops), (double)(bytes), s)
 
 extern "C" {
 
@@ -162,6 +203,10 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
 
 void dh_destroy(dh_handle* h) {
   if (!h) return;
+  for (auto& r : h->prof.recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
   if (h->params) (void)hipFree(h->params);
   if (h->norm) (void)hipFree(h->norm);
   delete h;
@@ -220,18 +265,36 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const Params& P = h->p;
   const int rows = nw * d.N * C;
   const int D = d.D;
-  launch_input(d, x, P.W0, w.h, w.geo, nw, C, s);
+  const double R = rows, DD = D, f4 = 4.0;
+  auto gemm = [&](const float* X, int ldx, const float* W, int ldw, const float* bias, const float* Res, int ldr,
+                  float* Y, int ldy, int ncols, int K) {
+    PROF(PK_GEMM, 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
+    launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
+  };
+  {
+    PROF(PK_INPUT, 8.0 * R * DD, f4 * R * DD);
+    launch_input(d, x, P.W0, w.h, w.geo, nw, C, s);
+  }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    launch_gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, rows, 3 * D, D, C, s);
-    launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);
+    gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    {
+      PROF(PK_ATTN, 0.0, f4 * R * 4.0 * DD);
+      launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);
+    }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
-    launch_gemm(w.o, D, lp.Wol, D, lp.bol, w.h, D, w.t, D, rows, D, D, C, s);
-    launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
-    launch_gemm(w.h, D, lp.Wm, D, lp.bm, nullptr, 0, w.o, D, rows, D, D, C, s);
-    launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
+    gemm(w.o, D, lp.Wol, D, lp.bol, w.h, D, w.t, D, D, D);
+    {
+      PROF(PK_LN, 0.0, f4 * R * 2.0 * DD);
+      launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
+    }
+    gemm(w.h, D, lp.Wm, D, lp.bm, nullptr, 0, w.o, D, D, D);
+    {
+      PROF(PK_LN, 0.0, f4 * R * 3.0 * DD);
+      launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
+    }
   }
-  launch_gemm(w.h, D, P.Worb, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, rows, d.orb_cols, D, C, s);
+  gemm(w.h, D, P.Worb, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
 
@@ -254,7 +317,10 @@ int dh_logpsi(dh_handle* h, const float* x, int B, float* logpsi, void* ws, size
   hipStream_t s = (hipStream_t)stream;
   Work w = carve(h->d, B, 1, ws);
   if (int rc = run_trunk(h, x, B, 1, w, s)) return rc;
-  launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, B, s);
+  {
+    PROF(PK_DET_VALUE, 0.0, 4.0 * B * h->d.N * h->d.ld_orb);
+    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, B, s);
+  }
   return check_launch();
 }
 
@@ -269,16 +335,28 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
   Work w = carve(d, B, 1, ws);
   // initial log-probability (mcmc.py:142)
   if (int rc = run_trunk(h, x, B, 1, w, s)) return rc;
-  launch_det_value(d, w.F, x, h->p.jastrow, h->norm, w.logpsi, B, s);
+  {
+    PROF(PK_DET_VALUE, 0.0, 4.0 * B * d.N * d.ld_orb);
+    launch_det_value(d, w.F, x, h->p.jastrow, h->norm, w.logpsi, B, s);
+  }
   launch_lp_from_logpsi(w.logpsi, lp, n_accept, B, s);
   const size_t nstride = (size_t)B * (2 * d.N + 1);
   for (int st = 0; st < steps; ++st) {
     const float* nz = noise ? noise + st * nstride : nullptr;
     const uint64_t step = counter + (uint64_t)st;
-    launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s);
+    {
+      PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
+      launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s);
+    }
     if (int rc = run_trunk(h, w.x2, B, 1, w, s)) return rc;
-    launch_det_value(d, w.F, w.x2, h->p.jastrow, h->norm, w.logpsi, B, s);
-    launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, step, walker_offset, nz, 0, s);
+    {
+      PROF(PK_DET_VALUE, 0.0, 4.0 * B * d.N * d.ld_orb);
+      launch_det_value(d, w.F, w.x2, h->p.jastrow, h->norm, w.logpsi, B, s);
+    }
+    {
+      PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
+      launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, step, walker_offset, nz, 0, s);
+    }
   }
   return check_launch();
 }
@@ -298,7 +376,10 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
     Work w = carve(d, nw, d.C, ws);
     const float* xc = x + (size_t)b0 * d.N * 2;
     if (int rc = run_trunk(h, xc, nw, d.C, w, s)) return rc;
-    launch_det_energy(d, w.F, xc, w.geo, h->p.jastrow, h->norm, e_l + 2 * (size_t)b0, obs + 8 * (size_t)b0, nw, s);
+    {
+      PROF(PK_DET_ENERGY, 0.0, 4.0 * nw * d.N * d.C * d.ld_orb);
+      launch_det_energy(d, w.F, xc, w.geo, h->p.jastrow, h->norm, e_l + 2 * (size_t)b0, obs + 8 * (size_t)b0, nw, s);
+    }
     if (int rc = check_launch()) return rc;
   }
   return DH_OK;
@@ -328,6 +409,30 @@ int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t
 size_t dh_debug_f_offset(const dh_handle* h, int B, int op) {
   Work w = carve(h->d, B, op == 1 ? h->d.C : 1, reinterpret_cast<void*>(size_t(64)));
   return (size_t)(w.F - reinterpret_cast<float*>(size_t(64)));
+}
+
+int dh_profile_enable(dh_handle* h, int on) {
+  if (!h) return fail(DH_EINVAL, "null handle");
+  h->prof.on = on != 0;
+  h->prof.used = 0;
+  return DH_OK;
+}
+
+int dh_profile_read(dh_handle* h, double* out, int reset) {
+  if (!h || !out) return fail(DH_EINVAL, "null argument");
+  for (int i = 0; i < 4 * PK_COUNT; ++i) out[i] = 0.0;
+  for (size_t i = 0; i < h->prof.used; ++i) {
+    ProfRec& r = h->prof.recs[i];
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    out[4 * r.kind + 0] += 1.0;
+    out[4 * r.kind + 1] += ms;
+    out[4 * r.kind + 2] += r.flops;
+    out[4 * r.kind + 3] += r.bytes;
+  }
+  if (reset) h->prof.used = 0;
+  return PK_COUNT;
 }
 
 int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream) {

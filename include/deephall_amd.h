@@ -94,7 +94,7 @@ const char* dh_version(void);
  *                              zero padded to ld_orb (multiple of 128)
  *   2+8L     borb [ld_orb]
  *   3+8L     jastrow [2]       ee_par, ee_anti
- * Returns the number of segments (3+8L) and writes up to `n` offsets; the
+ * Returns the number of segments (4+8L) and writes up to `n` offsets; the
  * total float count is offsets[nseg] (written if n > nseg). */
 int dh_param_layout(const dh_handle* h, size_t* offsets, int n);
 /* Copy the packed parameter buffer (device pointer, `count` floats) into the
@@ -155,6 +155,15 @@ int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int3
 /* Potential energy only (make_potential, hamiltonian.py:63-80), NOT multiplied by
  * interaction_strength: pe[B]. */
 int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream);
+
+/* Kernel timing with HIP events on the launch stream (bench / roofline).
+ * dh_profile_enable(h, 1) starts recording every kernel launch of this handle;
+ * dh_profile_read fills out[k*4 + {0,1,2,3}] = {launches, total ms, algorithmic
+ * FLOPs, algorithmic bytes} for kernel class k (returns the number of classes):
+ *   0 GEMM  1 attention  2 LayerNorm  3 input  4 det (log psi)  5 det (energy)
+ *   6 MCMC proposal/accept.  Synchronises on the recorded events. */
+int dh_profile_enable(dh_handle* h, int on);
+int dh_profile_read(dh_handle* h, double* out, int reset);
 
 /* Test hooks: run the network trunk + orbital GEMM only and leave the
  * activations in the workspace (trunk output at float offset 0, orbital

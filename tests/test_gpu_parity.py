@@ -1,0 +1,233 @@
+"""GPU parity of the HIP path (through the C ABI) against the float64 oracle.
+
+Tolerances (f32 kernels vs the f64 restatement; the reference itself is f32):
+  log psi      |d Re| <= 2e-5 * max(1, |Re|);  phase within 1e-4 (mod 2 pi)
+  E_L, KE      |d| <= 2e-4 * max(1, |ref|)     (complex)
+  Lz, Lz^2, L^2, PE  |d| <= 2e-4 * max(1, |ref|)
+Walkers are kept 0.15 rad from the poles (the cot/1/sin^2 terms of
+hamiltonian.py:121-129 amplify f32 rounding there, in the reference as well).
+"""
+
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from deephall_amd import config, hamiltonian, make_network
+from deephall_amd.loss import device_stats
+from deephall_amd.mcmc import make_mcmc_step
+from deephall_amd.random import Key
+from deephall_amd.train import init_guess
+from helpers import make_params, make_walkers, oracle_config, rel_err, to_device_params
+from oracle import channels as CH
+from oracle import philox
+from oracle import reference as R
+from test_oracle_kat import droplet_L2, engineered_params
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+TOL_E = 2e-4
+
+
+def build(ocfg):
+    system = config.System(
+        nspins=tuple(ocfg.nspins), flux=ocfg.flux, interaction_strength=ocfg.interaction_strength,
+        interaction_type=config.InteractionType(ocfg.interaction_type), radius=ocfg.radius,
+    )
+    net = config.Network()
+    net.psiformer.num_heads, net.psiformer.heads_dim = ocfg.num_heads, ocfg.heads_dim
+    net.psiformer.num_layers, net.psiformer.determinants = ocfg.num_layers, ocfg.determinants
+    return system, make_network(system, net)
+
+
+def phase_err(a, b):
+    d = np.angle(np.exp(1j * (np.asarray(a) - np.asarray(b))))
+    return float(np.max(np.abs(d)))
+
+
+def check_energy(e, o, ref_e, ref_o, tol=TOL_E):
+    assert rel_err(e.cpu().numpy(), ref_e) < tol
+    assert rel_err(o["kinetic"].cpu().numpy(), ref_o["kinetic"]) < tol
+    for k, rk in (("potential", "potential"), ("angular_momentum_z", "angular_momentum_z"),
+                  ("angular_momentum_z_square", "angular_momentum_z_square"),
+                  ("angular_momentum_square", "angular_momentum_square")):
+        assert rel_err(o[k].cpu().numpy(), ref_o[rk]) < tol, k
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "MIX"])
+def test_golden_local_energy(cuda, name):
+    g = np.load(GOLDEN / f"local_energy_{name}.npz")
+    ocfg = R.OracleConfig(**json.loads(str(g["config"])))
+    ocfg.nspins = tuple(ocfg.nspins)
+    p64 = make_params(ocfg, seed=int(g["param_seed"]))
+    system, model = build(ocfg)
+    params = to_device_params(p64)
+    x = torch.tensor(g["x"], device=cuda)
+    lp = model.apply(params, x).cpu().numpy()
+    assert rel_err(lp.real, g["logpsi"].real) < 2e-5
+    assert phase_err(lp.imag, g["logpsi"].imag) < 1e-4
+    e, o = hamiltonian.local_energy(model, system)(params, x)
+    ref_o = {"kinetic": g["kinetic"], "potential": g["potential"], "angular_momentum_z": g["lz"],
+             "angular_momentum_z_square": g["lz2"], "angular_momentum_square": g["l2"]}
+    check_energy(e, o, g["e_l"], ref_o)
+
+
+@pytest.mark.parametrize("name,B", [("C2", 16), ("C4", 4), ("C5", 2)])
+def test_local_energy_vs_channel_oracle(cuda, name, B):
+    ocfg = oracle_config(name)
+    p64 = make_params(ocfg)
+    system, model = build(ocfg)
+    params = to_device_params(p64)
+    x = make_walkers(B, ocfg.nelec, seed=11)
+    lp_ref, ke, o_ref, _ = CH.local_energy(p64, ocfg, torch.tensor(x, dtype=torch.float64))
+    pe = np.array([R.potential(ocfg, torch.tensor(x[b], dtype=torch.float64)).item() for b in range(B)])
+    e, o = hamiltonian.local_energy(model, system)(params, torch.tensor(x, device=cuda))
+    ref_o = {k: v.numpy() for k, v in o_ref.items()}
+    ref_o["kinetic"] = ke.numpy()
+    ref_o["potential"] = pe
+    check_energy(e, o, ke.numpy() + pe, ref_o, tol=5e-4 if name == "C5" else TOL_E)
+    lp = model.apply(params, torch.tensor(x, device=cuda)).cpu().numpy()
+    assert rel_err(lp.real, lp_ref.numpy().real) < 2e-5
+
+
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_engineered_known_answer_full_batch(cuda, name):
+    """Every walker of a full batch: KE = N/2, Lz, L^2 of the LLL droplet (analytic pin)."""
+    ocfg = oracle_config(name, interaction_strength=0.0)
+    p = engineered_params(ocfg)
+    system, model = build(ocfg)
+    params = to_device_params(p)
+    B = 4096 if name == "C2" else 512
+    x = torch.tensor(make_walkers(B, ocfg.nelec, seed=3, margin=0.3), device=cuda)
+    e, o = hamiltonian.local_energy(model, system)(params, x)
+    L2, Lz = droplet_L2(ocfg.nelec, ocfg.flux)
+    ke = o["kinetic"].cpu().numpy()
+    assert np.max(np.abs(ke - ocfg.nelec / 2)) < 1e-3 * ocfg.nelec
+    assert np.max(np.abs(o["angular_momentum_z"].cpu().numpy() - Lz)) < 1e-3 * max(1, abs(Lz))
+    assert np.max(np.abs(o["angular_momentum_square"].cpu().numpy() - L2)) < 2e-3 * max(1, L2)
+    assert np.max(np.abs(o["angular_momentum_z_square"].cpu().numpy() - Lz * Lz)) < 2e-3 * max(1, Lz * Lz)
+
+
+def test_batch_composition_and_chunking_invariance(cuda):
+    ocfg = oracle_config("C2")
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg))
+    x = torch.tensor(make_walkers(37, ocfg.nelec, seed=5), device=cuda)
+    lp_all = model.apply(params, x)
+    lp_part = torch.cat([model.apply(params, x[:5]), model.apply(params, x[5:])])
+    assert torch.equal(lp_all, lp_part)  # rows are independent: bit-identical
+    from deephall_amd.hamiltonian import _run_local_energy
+
+    e1, o1 = _run_local_energy(model, params, x)
+    h = model.prepare(params, x.device)
+    one = h.lib.dh_workspace_bytes(h.h, 4, 1)
+    e2, o2 = _run_local_energy(model, params, x, ws_budget=one)  # forces chunks of <= 4 walkers
+    assert torch.equal(e1, e2) and torch.equal(o1, o2)
+
+
+def test_nan_and_edge_walkers_propagate(cuda):
+    ocfg = oracle_config("C1")
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg))
+    x = torch.tensor(make_walkers(3, 3), device=cuda)
+    x[1, 0, 0] = float("nan")
+    e, o = hamiltonian.local_energy(model, system)(params, x)
+    lp = model.apply(params, x)
+    assert torch.isnan(e[1]).item() and torch.isnan(lp[1]).item()
+    assert torch.isfinite(e[0]).item() and torch.isfinite(e[2]).item()
+    e1, _ = hamiltonian.local_energy(model, system)(params, x[:1])  # B = 1
+    assert torch.equal(e1, e[:1])
+
+
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_golden_mcmc_injected_noise(cuda, name):
+    g = np.load(GOLDEN / f"mcmc_{name}.npz")
+    ocfg = R.OracleConfig(**json.loads(str(g["config"])))
+    ocfg.nspins = tuple(ocfg.nspins)
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg))
+    noise = torch.tensor(g["noise"], device=cuda)
+    steps, B = noise.shape[:2]
+    step = make_mcmc_step(model, batch_per_device=B, steps=steps)
+    x = torch.tensor(g["x0"], device=cuda)
+    x, pmove = step(params, x, Key(0), float(g["width"]), noise=noise)
+    assert np.array_equal(step.last_n_accept.cpu().numpy(), g["n_acc"])
+    assert np.max(np.abs(x.cpu().numpy() - g["x"])) < 2e-5
+    assert float(pmove) == pytest.approx(g["n_acc"].sum() / (steps * B))
+    assert rel_err(step.last_lp.cpu().numpy(), g["lp"]) < 2e-5
+
+
+def test_device_rng_matches_philox_oracle(cuda):
+    """The device draws exactly oracle/philox.py's numbers (integer part bit-exact)."""
+    N, B, seed = 6, 64, 1234
+    x = init_guess(Key(seed), B, N, cuda, walker_offset=100)
+    u1, u2 = philox.init_uniforms(seed, np.arange(100, 100 + B), N)
+    ref = R.init_guess_from_uniforms(u1.astype(np.float64), u2.astype(np.float64))
+    assert np.max(np.abs(x.cpu().numpy() - ref)) < 1e-5
+    # MCMC with device RNG == MCMC with the oracle's Philox noise injected
+    ocfg = oracle_config("C2")
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg))
+    x0 = torch.tensor(make_walkers(B, N, seed=9), device=cuda)
+    steps = 3
+    noise = []
+    for s in range(steps):
+        n, u, a = philox.mcmc_noise(seed, 50 + s, np.arange(B) + 7, N)
+        noise.append(np.concatenate([n, u, a[:, None]], -1))
+    noise = torch.tensor(np.stack(noise), dtype=torch.float32, device=cuda)
+    step = make_mcmc_step(model, batch_per_device=B, steps=steps)
+    xa, _ = step(params, x0.clone(), Key(seed, 50), 0.2, walker_offset=7)
+    na = step.last_n_accept.clone()
+    xb, _ = step(params, x0.clone(), Key(seed, 50), 0.2, noise=noise, walker_offset=7)
+    nb = step.last_n_accept.clone()
+    agree = (na == nb).float().mean().item()
+    assert agree > 0.95  # Box-Muller in f32 vs f64: rare borderline decisions may flip
+    same = (na == nb).cpu().numpy()
+    assert np.max(np.abs((xa - xb).cpu().numpy()[same])) < 1e-4
+
+
+def test_mcmc_sharding_invariance(cuda):
+    """Two 'ranks' with walker offsets reproduce one rank with all walkers (bit-exact)."""
+    ocfg = oracle_config("C1")
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg))
+    B = 64
+    x = torch.tensor(make_walkers(B, 3, seed=2), device=cuda)
+    full = make_mcmc_step(model, batch_per_device=B, steps=5)
+    half = make_mcmc_step(model, batch_per_device=B // 2, steps=5)
+    xa, _ = full(params, x.clone(), Key(99, 3), 0.1, walker_offset=0)
+    x0 = x[: B // 2].clone()
+    x1 = x[B // 2 :].clone()
+    half(params, x0, Key(99, 3), 0.1, walker_offset=0)
+    half(params, x1, Key(99, 3), 0.1, walker_offset=B // 2)
+    assert torch.equal(xa, torch.cat([x0, x1]))
+
+
+def test_energy_stats_kernel(cuda):
+    ocfg = oracle_config("C1")
+    system, model = build(ocfg)
+    g = np.random.default_rng(0)
+    B = 1000
+    e = g.standard_normal((B, 2)).astype(np.float32)
+    e[:, 0] += 3.0
+    e[7, 0] = 1e6  # outlier gets clipped
+    e[9, 1] = np.nan  # NaN walker excluded from the nanmeans
+    obs = g.standard_normal((B, 8)).astype(np.float32)
+    nacc = g.integers(0, 11, B).astype(np.int32)
+    out = device_stats(model, torch.tensor(e, device=cuda), torch.tensor(obs, device=cuda),
+                       torch.tensor(nacc, device=cuda), steps=10).cpu().numpy()
+    el = e[:, 0].astype(np.float64) + 1j * e[:, 1]
+    o = {"kinetic": obs[:, 0] + 1j * obs[:, 1], "potential": obs[:, 2]}
+    ref = R.loss_stats(el, o)
+    assert out[0] == pytest.approx(ref["energy"].real, rel=1e-5)
+    assert out[1] == pytest.approx(ref["energy"].imag, abs=1e-5)
+    assert out[2] == pytest.approx(ref["clipped_energy"].real, rel=1e-5)
+    assert out[3] == pytest.approx(ref["clipped_energy"].imag, abs=1e-5)
+    assert out[4] == pytest.approx(np.nanmean(el.real**2), rel=1e-5)
+    assert out[5] == pytest.approx(obs[:, 0].mean(), abs=1e-5)
+    assert out[11] == pytest.approx(nacc.sum() / (10 * B), rel=1e-6)
+    assert out[12] == B - 1
