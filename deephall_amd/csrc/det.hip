@@ -39,9 +39,13 @@ struct FView {
 struct EnvLeaf {
   cf e0, dth, dph, lb, d2th;
 };
-__device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves) {
+// `gauge` = sigma * Q removes the per-electron phase exp(i sigma Q phi) from the envelope
+// (north patch sigma = +1, south patch sigma = -1; 0 = reference gauge).  The network
+// channels then stay regular near the poles; the removed term i Q sum sigma phi is
+// added back analytically (in double) by the energy assembly.
+__device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves, float gauge = 0.f) {
   const int a = p, b = M - 1 - p;
-  const float m = 0.5f * (float)(a - b);
+  const float m = 0.5f * (float)(a - b) - gauge;
   float c, s;
   sincosf(0.5f * th, &s, &c);
   float sph, cph;
@@ -355,7 +359,8 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
   }
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
-    const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true);
+    const float gauge = (geo[4 * i + 1] >= 0.f ? Q : -Q);
+    const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true, gauge);
     E0[idx] = e.e0;
     DTH[idx] = e.dth;
     DPH[idx] = e.dph;
@@ -477,7 +482,7 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
         const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
         cf acc{0.f, 0.f};
         for (int p = 0; p < M; ++p) {
-          const float m = (float)p - 0.5f * (float)(M - 1);
+          const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
           const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
           cfma(acc, F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
           cfma(acc, F.at(r0, blk, p, j, kd), sf);
@@ -591,6 +596,21 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
       }
     }
     if (interaction == DH_INTERACTION_COULOMB) pe /= (double)radius;
+    // gauge term A = i Q sum_i sigma_i phi_i (env_leaf): tangents, flow channels, phase
+    double gauge_phase = 0.0;
+    for (int i = 0; i < N; ++i) {
+      const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+      const double sg = (geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0;
+      tg_im[2 * i + 1] += Q * sg / st;
+      gauge_phase += Q * sg * (double)x[2 * (b * N + i) + 1];
+      const double cot = ct / st;
+      // phi acceleration along the three rotation flows (see env_flow2)
+      const double tdot[3] = {-sp, cp, 0.0};
+      const double thp[3] = {cp * cot, sp * cot, -1.0};
+      const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
+      const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
+      for (int kk = 0; kk < 3; ++kk) S_im[kk] += Q * sg * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
+    }
     pe *= (double)lambda;
     LB_re += Jlb;
     // assembly
@@ -642,7 +662,7 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
     ob[4] = (float)lz2;
     ob[5] = (float)L2;
     ob[6] = (float)(val_re + J);
-    ob[7] = (float)val_im;
+    ob[7] = (float)remainder(val_im + gauge_phase, 2.0 * M_PI);
   }
 }
 

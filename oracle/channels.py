@@ -31,6 +31,10 @@ from .reference import OracleConfig
 DT = torch.float64
 
 
+def _ctype(x):
+    return torch.complex128 if x.dtype == torch.float64 else torch.complex64
+
+
 def n_channels(N):
     return 2 * N + 5
 
@@ -188,7 +192,12 @@ def attention_ch(Qc, Kc, Vc, alpha):
 # ------------------------------------------------------------------ envelope / Jastrow leaves
 
 
-def envelope_channels(x, Q):
+def gauge_sign(x):
+    """North (+1) / south (-1) patch of each electron: the gauge the kernels use."""
+    return torch.where(torch.cos(x[..., 0]) >= 0, 1.0, -1.0).to(x.dtype)
+
+
+def envelope_channels(x, Q, gauge=False):
     """Envelope env[i,m] = c_m u^(Q+m) v^(Q-m) and its leaf derivatives.
 
     Returns complex [B,N,M] tensors: e0, dth (d/dtheta), dph (d/dphi / sin theta),
@@ -198,10 +207,12 @@ def envelope_channels(x, Q):
     g = geometry(x)
     th, ph, st, ct = g["th"], g["ph"], g["st"], g["ct"]
     M = int(round(2 * Q)) + 1
-    a = torch.arange(M, dtype=DT)  # Q+m
+    a = torch.arange(M, dtype=x.dtype)  # Q+m
     b = (M - 1) - a  # Q-m
     m = a - Q
-    norm = torch.tensor(np.sqrt(ss.comb(2 * Q, Q - np.arange(-Q, Q + 1))), dtype=DT)
+    if gauge:  # env * exp(-i sigma Q phi): regular near the electron's own pole
+        m = m - (gauge_sign(x) * Q)[..., None]
+    norm = torch.tensor(np.sqrt(ss.comb(2 * Q, Q - np.arange(-Q, Q + 1))), dtype=x.dtype)
     c = torch.cos(th / 2)[..., None]
     s = torch.sin(th / 2)[..., None]
 
@@ -218,7 +229,7 @@ def envelope_channels(x, Q):
         - a * (b + 1) * pw(c, a) * pw(s, b)
         + a * (a - 1) * pw(c, a - 2) * pw(s, b + 2)
     )
-    phase = torch.exp(1j * m * ph[..., None].to(torch.complex128))
+    phase = torch.exp(1j * m * ph[..., None].to(_ctype(x)))
     e0 = norm * R * phase
     d_th = norm * R1 * phase
     d_ph = 1j * m * e0  # d/dphi
@@ -252,9 +263,9 @@ def jastrow_channels(x, nspins, a_par, a_anti):
     g = geometry(x)
     B, N = x.shape[:2]
     rh, thh, phh = g["r_hat"], g["th_hat"], g["ph_hat"]
-    J = torch.zeros(B, dtype=DT)
-    grad = torch.zeros(B, 2 * N, dtype=DT)
-    lb = torch.zeros(B, dtype=DT)
+    J = torch.zeros(B, dtype=x.dtype)
+    grad = torch.zeros(B, 2 * N, dtype=x.dtype)
+    lb = torch.zeros(B, dtype=x.dtype)
     n_up = nspins[0]
     for i in range(N):
         for j in range(i + 1, N):
@@ -310,7 +321,7 @@ def trunk_channels(params, cfg: OracleConfig, x):
     return X, inter
 
 
-def local_energy(params, cfg: OracleConfig, x):
+def local_energy(params, cfg: OracleConfig, x, gauge=False):
     """Batched E_L by channel propagation. x [B,N,2] float64.
 
     Returns (logpsi [B] complex, E_L [B] complex, obs dict, raw dict)."""
@@ -338,10 +349,10 @@ def local_energy(params, cfg: OracleConfig, x):
     if cfg.nspins[1] > 0:
         parts.append(orb(1, Xh[:, n_up:]))
     F = torch.cat(parts, 1)  # [B,N(i),C,M,N(j),K]
-    e0, dth, dph, elb, esf = envelope_channels(x, Q)  # [B,N,M]
+    e0, dth, dph, elb, esf = envelope_channels(x, Q, gauge)  # [B,N,M]
     ctr = lambda Fc, e: torch.einsum("bimjk,bim->bkij", Fc, e)  # noqa: E731
     Phi0 = ctr(F[:, :, 0], e0)  # [B,K,N,N]
-    Phit = torch.zeros(x.shape[0], T, K, N, N, dtype=torch.complex128)
+    Phit = torch.zeros(x.shape[0], T, K, N, N, dtype=_ctype(x))
     for t in range(T):
         i = t // 2
         de = dth if t % 2 == 0 else dph
@@ -361,7 +372,7 @@ def local_energy(params, cfg: OracleConfig, x):
     ell_t = tr(Mt)  # [B,T,K]
     ell_L = tr(torch.einsum("bkij,bkjl->bkil", Binv, PhiL)) - tr(Mt @ Mt).sum(1)
     ell_S = []
-    alc = alpha.to(torch.complex128)
+    alc = alpha.to(_ctype(x))
     for k in range(3):
         flow1 = g["ph_hat"][..., k, None] * dth - g["th_hat"][..., k, None] * dph  # [B,N,M]
         Fu = torch.einsum("bt,bitmjl->bimjl", alc[:, k], F[:, :, 1 : 1 + T])
@@ -384,6 +395,18 @@ def local_energy(params, cfg: OracleConfig, x):
     J, Jg, Jlb = jastrow_channels(x, cfg.nspins, params["Jastrow_0/ee_par"][0], params["Jastrow_0/ee_anti"][0])
     logpsi = val + J
     tg = g1 + Jg
+    if gauge:  # add back A = i Q sum_i sigma_i phi_i analytically
+        sg = gauge_sign(x)
+        st_, ct_, sp_, cp_ = g["st"], g["ct"], g["sp"], g["cp"]
+        cot_ = ct_ / st_
+        logpsi = logpsi + 1j * Q * (sg * x[..., 1]).sum(-1)
+        tg = tg.clone()
+        tg[:, 1::2] = tg[:, 1::2] + 1j * Q * sg / st_
+        tdot = [-sp_, cp_, torch.zeros_like(sp_)]
+        thp = [cp_ * cot_, sp_ * cot_, -torch.ones_like(sp_)]
+        d_th = [-cp_ / st_**2, -sp_ / st_**2, torch.zeros_like(sp_)]
+        d_ph = [-sp_ * cot_, cp_ * cot_, torch.zeros_like(sp_)]
+        S = S + torch.stack([(1j * Q * sg * (-(d_th[k] * tdot[k] - d_ph[k] * thp[k]))).sum(-1) for k in range(3)], -1)
     LB = LB + Jlb
     # assembly (hamiltonian.py:115-169, rewritten through the channels)
     st, ct, sp, cp = g["st"], g["ct"], g["sp"], g["cp"]

@@ -51,6 +51,35 @@ def to_device_params(p):
     return {k: v.float().cuda() for k, v in p.items()}
 
 
+def cancellation_scales(p64, cfg, x):
+    """Per-walker magnitude of the terms that cancel in each observable (float64
+    channel oracle).  f32 results — the reference's and ours — are accurate
+    relative to these, not to the (possibly much smaller) result:
+      KE  = (-LB - sum t^2 + Mag) / 2r^2
+      L^2 = -sum_k [S_k + (G_k + i M_k)^2],  Lz^2 = -Re(S_z + G_z^2)."""
+    from oracle import channels as CH
+
+    xt = torch.as_tensor(x, dtype=torch.float64)
+    _, ke, obs, raw = CH.local_energy(p64, cfg, xt)
+    th, ph = xt[..., 0], xt[..., 1]
+    Q = cfg.Q
+    cot = torch.cos(th) / torch.sin(th)
+    t = raw["t"]
+    mag = ((Q * cot) ** 2).sum(-1) + (2 * Q * cot.abs() * t[:, 1::2].abs()).sum(-1)
+    ke_s = (raw["LB"].abs() + (t.abs() ** 2).sum(-1) + mag) / (2 * cfg.r**2)
+    Mv = torch.stack([Q * (torch.cos(ph) / torch.sin(th)).sum(-1), Q * (torch.sin(ph) / torch.sin(th)).sum(-1),
+                      torch.zeros_like(th[:, 0])], -1)
+    l2_s = (raw["S"].abs() + (raw["G"] + 1j * Mv).abs() ** 2).sum(-1)
+    lz2_s = raw["S"][:, 2].abs() + raw["G"][:, 2].abs() ** 2
+    return {"kinetic": ke_s.numpy(), "angular_momentum_square": l2_s.numpy(),
+            "angular_momentum_z_square": lz2_s.numpy(), "angular_momentum_z": raw["G"][:, 2].abs().numpy()}
+
+
+def scaled_err(a, b, scale):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b) / np.maximum(np.maximum(np.abs(b), 1.0), np.asarray(scale))))
+
+
 def rel_err(a, b, floor=1.0):
     a = np.asarray(a)
     b = np.asarray(b)
