@@ -411,6 +411,14 @@ size_t dh_debug_f_offset(const dh_handle* h, int B, int op) {
   return (size_t)(w.F - reinterpret_cast<float*>(size_t(64)));
 }
 
+// Test hook: one GEMM launch of kernel variant `variant` (-1 = default).
+int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
+                  int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream) {
+  launch_gemm_variant(variant < 0 ? 0 : variant, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
+                      (hipStream_t)stream);
+  return check_launch();
+}
+
 int dh_profile_enable(dh_handle* h, int on) {
   if (!h) return fail(DH_EINVAL, "null handle");
   h->prof.on = on != 0;

@@ -41,7 +41,7 @@ struct Pass {
   int rows_pad;
 };
 
-constexpr int kRowPad = 128;
+constexpr int kRowPad = 256;
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
@@ -56,6 +56,9 @@ inline void ensure_smem(Kern kernel, size_t bytes) {
 // gemm.hip: Y[r][n] = sum_k X[r][k] W[k][n] + (r % C == 0 ? bias[n] : 0) + (R ? R[r][n] : 0)
 void launch_gemm(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R, int ldr,
                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+void launch_gemm_variant(int v, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
+                         int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+void set_gemm_variant(int v);
 
 // input.hip
 // Features (psiformer.py:51-60) of every channel times W0 -> h [rows][D]; also

@@ -195,10 +195,64 @@ __global__ void layernorm_kernel(const float* X, const float* __restrict__ Z, co
   }
 }
 
+// Value-only rows (log psi / MCMC, C == 1): one wave per row, D = 256 * V floats,
+// float4 per lane, two-pass mean/variance in registers.  Pure HBM streaming.
+template <int V>
+__global__ __launch_bounds__(256) void layernorm_value_kernel(const float* X, const float* __restrict__ Z,
+                                                              const float* __restrict__ ln, float* h, int rows,
+                                                              int mode) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  constexpr int D = 256 * V;
+  const size_t b4 = (size_t)row * (D / 4);
+  float4 v[V];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const size_t q = b4 + lane + 64 * j;
+    if (mode == 0) {
+      v[j] = reinterpret_cast<const float4*>(X)[q];
+    } else {
+      const float4 z = reinterpret_cast<const float4*>(Z)[q];
+      const float4 r = reinterpret_cast<const float4*>(h)[q];
+      v[j] = make_float4(r.x + tanhf(z.x), r.y + tanhf(z.y), r.z + tanhf(z.z), r.w + tanhf(z.w));
+    }
+    sum += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  }
+  const float mean = wave_sum(sum) * (1.f / D);
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    v[j].x -= mean;
+    v[j].y -= mean;
+    v[j].z -= mean;
+    v[j].w -= mean;
+    sq += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+  }
+  const float s = 1.f / sqrtf(wave_sum(sq) * (1.f / D) + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c4 = lane + 64 * j;
+    const float4 g = reinterpret_cast<const float4*>(ln)[c4];
+    const float4 bb = reinterpret_cast<const float4*>(ln + D)[c4];
+    reinterpret_cast<float4*>(h)[b4 + c4] =
+        make_float4(g.x * (s * v[j].x) + bb.x, g.y * (s * v[j].y) + bb.y, g.z * (s * v[j].z) + bb.z,
+                    g.w * (s * v[j].w) + bb.w);
+  }
+}
+
 }  // namespace
 
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
                       int nw, int C, int mode, hipStream_t s) {
+  if (C == 1 && (d.D == 256 || d.D == 512)) {
+    const int rows = nw * d.N;
+    if (d.D == 256)
+      hipLaunchKernelGGL(layernorm_value_kernel<1>, dim3((rows + 3) / 4), dim3(256), 0, s, X, Z, ln, h, rows, mode);
+    else
+      hipLaunchKernelGGL(layernorm_value_kernel<2>, dim3((rows + 3) / 4), dim3(256), 0, s, X, Z, ln, h, rows, mode);
+    return;
+  }
   const bool ch = C > 1;
   const size_t floats = (size_t)C * d.D + (ch ? 3 * d.D + 3 * d.T : 0) + 2 * C + d.T + 4 + 8;
   const int threads = 256;

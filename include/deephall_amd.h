@@ -170,6 +170,10 @@ int dh_profile_read(dh_handle* h, double* out, int reset);
  * features at float offset dh_debug_f_offset). */
 int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t ws_bytes, void* stream);
 size_t dh_debug_f_offset(const dh_handle* h, int B, int op);
+/* Test hook: one launch of GEMM kernel variant `variant` (-1 = default):
+ * Y = X W (+ bias on rows r % C == 0) (+ R).  X must hold round_up(rows, 256) rows. */
+int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
+                  int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream);
 
 /* init_guess with the device RNG: theta = arccos U(-1,1), phi = U(-pi,pi). */
 int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream);
