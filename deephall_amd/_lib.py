@@ -50,7 +50,8 @@ EXPORTS = [
 ]
 
 
-PROF_KINDS = ["gemm", "attention", "layernorm", "input", "det_value", "det_energy", "mcmc"]
+PROF_KINDS = ["gemm", "attention", "layernorm", "input", "det_value", "det_energy", "mcmc",
+              "gemm_ch", "attention_ch", "layernorm_ch", "input_ch"]
 
 
 class DhConfig(C.Structure):

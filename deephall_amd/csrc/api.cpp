@@ -76,6 +76,8 @@ Work carve(const Dims& d, int nw, int C, void* base) {
 
 // Optional per-kernel HIP-event timing (bench.py reads it to compute the live roofline).
 enum ProfKind { PK_GEMM = 0, PK_ATTN, PK_LN, PK_INPUT, PK_DET_VALUE, PK_DET_ENERGY, PK_MCMC, PK_COUNT };
+// channel-mode (C > 1) launches of GEMM/attention/LayerNorm/input are recorded as kind + PK_CH
+constexpr int PK_CH = PK_COUNT, PK_TOTAL = PK_COUNT + 4;
 struct ProfRec {
   hipEvent_t a, b;
   int kind;
@@ -268,29 +270,29 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const double R = rows, DD = D, f4 = 4.0;
   auto gemm = [&](const float* X, int ldx, const float* W, int ldw, const float* bias, const float* Res, int ldr,
                   float* Y, int ldy, int ncols, int K) {
-    PROF(PK_GEMM, 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
+    PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
     launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
   };
   {
-    PROF(PK_INPUT, 8.0 * R * DD, f4 * R * DD);
+    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD, f4 * R * DD);
     launch_input(d, x, P.W0, w.h, w.geo, nw, C, s);
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
     gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
-      PROF(PK_ATTN, 0.0, f4 * R * 4.0 * DD);
+      PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 4.0 * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
     gemm(w.o, D, lp.Wol, D, lp.bol, w.h, D, w.t, D, D, D);
     {
-      PROF(PK_LN, 0.0, f4 * R * 2.0 * DD);
+      PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
       launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
     }
     gemm(w.h, D, lp.Wm, D, lp.bm, nullptr, 0, w.o, D, D, D);
     {
-      PROF(PK_LN, 0.0, f4 * R * 3.0 * DD);
+      PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 3.0 * DD);
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
@@ -428,7 +430,7 @@ int dh_profile_enable(dh_handle* h, int on) {
 
 int dh_profile_read(dh_handle* h, double* out, int reset) {
   if (!h || !out) return fail(DH_EINVAL, "null argument");
-  for (int i = 0; i < 4 * PK_COUNT; ++i) out[i] = 0.0;
+  for (int i = 0; i < 4 * PK_TOTAL; ++i) out[i] = 0.0;
   for (size_t i = 0; i < h->prof.used; ++i) {
     ProfRec& r = h->prof.recs[i];
     HIP_TRY(hipEventSynchronize(r.b));
@@ -440,7 +442,7 @@ int dh_profile_read(dh_handle* h, double* out, int reset) {
     out[4 * r.kind + 3] += r.bytes;
   }
   if (reset) h->prof.used = 0;
-  return PK_COUNT;
+  return PK_TOTAL;
 }
 
 int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream) {

@@ -289,9 +289,592 @@ __global__ void attention_kernel(const float* __restrict__ qkv, const float* __r
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Channel kernel v2: one 256-thread workgroup per (walker, head); channel c+1's q/k/v are
+// prefetched into registers (PF float4 per thread) while channel c is computed, then
+// committed to the other half of a double-buffered LDS image: 3 barriers per channel,
+// 4 lanes per score pair.
+struct AttnSmem2 {
+  int alpha, q0, k0, v0, qc, kc, vc, A0, S, P, R, accS, T2, SuB, Au, accOL, qu, ku, vu, total;
+};
+__host__ __device__ inline AttnSmem2 attn_layout2(int N, int dh) {
+  AttnSmem2 L;
+  const int ld = dh + 1, nd = N * ld, nn = N * N, T = 2 * N;
+  int o = 0;
+  L.alpha = o;
+  o += 3 * T + 4;
+  L.q0 = o;
+  o += nd;
+  L.k0 = o;
+  o += nd;
+  L.v0 = o;
+  o += nd;
+  L.qc = o;
+  o += 2 * nd;
+  L.kc = o;
+  o += 2 * nd;
+  L.vc = o;
+  o += 2 * nd;
+  L.A0 = o;
+  o += nn;
+  L.S = o;
+  o += nn;
+  L.P = o;
+  o += nn;
+  L.R = o;
+  o += nn;
+  L.accS = o;
+  o += nn;
+  L.T2 = o;
+  o += nn;
+  L.SuB = o;
+  o += 3 * nn;
+  L.Au = o;
+  o += 3 * nn;
+  L.accOL = o;
+  o += nd;
+  L.qu = o;
+  o += 3 * nd;
+  L.ku = o;
+  o += 3 * nd;
+  L.vu = o;
+  o += 3 * nd;
+  L.total = o;
+  return L;
+}
+
+template <int PF, int RPT>
+__global__ __launch_bounds__(256) void attention_ch_kernel(const float* __restrict__ qkv,
+                                                           const float* __restrict__ geo, float* __restrict__ o,
+                                                           int N, int H, int dh) {
+  extern __shared__ float sm[];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int C = 2 * N + 5, T = 2 * N, D = H * dh, ld = dh + 1, nd = N * ld, nn = N * N;
+  const AttnSmem2 L = attn_layout2(N, dh);
+  const float scale = 1.0f / sqrtf((float)dh);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  float *al = sm + L.alpha, *q0 = sm + L.q0, *k0 = sm + L.k0, *v0 = sm + L.v0;
+  float *A0 = sm + L.A0, *S = sm + L.S, *P = sm + L.P, *Rm = sm + L.R;
+  float *accS = sm + L.accS, *T2 = sm + L.T2, *SuB = sm + L.SuB, *Au = sm + L.Au;
+  float *accOL = sm + L.accOL, *qu = sm + L.qu, *ku = sm + L.ku, *vu = sm + L.vu;
+  const int dq = dh >> 2, nf4 = N * dq, tot4 = 3 * nf4;
+
+  float4 pf[PF];
+  auto prefetch = [&](int c) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      const int f = tid + s * 256;
+      if (f < tot4) {
+        const int mat = f / nf4, g = f - mat * nf4, i = g / dq, d4 = g - i * dq;
+        pf[s] = *reinterpret_cast<const float4*>(qkv + ((size_t)(b * N + i) * C + c) * (3 * D) + mat * D + h * dh +
+                                                 4 * d4);
+      }
+    }
+  };
+  auto commit = [&](float* qd, float* kd, float* vd) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      const int f = tid + s * 256;
+      if (f < tot4) {
+        const int mat = f / nf4, g = f - mat * nf4, i = g / dq, d4 = g - i * dq;
+        float* dst = (mat == 0 ? qd : (mat == 1 ? kd : vd)) + i * ld + 4 * d4;
+        dst[0] = pf[s].x;
+        dst[1] = pf[s].y;
+        dst[2] = pf[s].z;
+        dst[3] = pf[s].w;
+      }
+    }
+  };
+  auto store_o = [&](int c, int i, int d, float val) { o[((size_t)(b * N + i) * C + c) * D + h * dh + d] = val; };
+  // 4 lanes per (i, j) pair: partial dot products over quarters of dh, reduced by shuffles
+  auto dots = [&](const float* qa, const float* kb, const float* qb, const float* ka, const float* qx,
+                  const float* kx, int p, float& s1, float& s2) {
+    const int pair = p >> 2, qt = p & 3;
+    const int i = pair / N, j = pair - (pair / N) * N;
+    const int d0 = qt * dq;
+    s1 = 0.f;
+    s2 = 0.f;
+    for (int d = d0; d < d0 + dq; ++d) {
+      s1 = fmaf(qa[i * ld + d], kb[j * ld + d], s1);
+      if (qb) s1 = fmaf(qb[i * ld + d], ka[j * ld + d], s1);
+      if (qx) s2 = fmaf(qx[i * ld + d], kx[j * ld + d], s2);
+    }
+    s1 += __shfl_xor(s1, 1, 64);
+    s1 += __shfl_xor(s1, 2, 64);
+    s2 += __shfl_xor(s2, 1, 64);
+    s2 += __shfl_xor(s2, 2, 64);
+  };
+
+  for (int t = tid; t < T; t += nt) {
+    const int i = t >> 1;
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((t & 1) == 0)
+        a = (k == 0) ? -g.z : (k == 1 ? g.w : 0.f);
+      else
+        a = (k == 0) ? -(g.y * g.w) : (k == 1 ? -(g.y * g.z) : g.x);
+      al[k * T + t] = a;
+    }
+  }
+  prefetch(0);
+  commit(q0, k0, v0);
+  prefetch(1);
+  for (int p = tid; p < nn; p += nt) {
+    accS[p] = 0.f;
+    T2[p] = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      SuB[k * nn + p] = 0.f;
+      Au[k * nn + p] = 0.f;
+    }
+  }
+  const int d_own = tid & 63, g_own = tid >> 6;
+  float rOL[RPT], rQu[3][RPT], rKu[3][RPT], rVu[3][RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    rOL[r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) rQu[kk][r] = rKu[kk][r] = rVu[kk][r] = 0.f;
+  }
+  __syncthreads();
+  // ---- value channel
+  for (int p = tid; p < 4 * nn; p += nt) {
+    float s1, s2;
+    dots(q0, k0, nullptr, nullptr, nullptr, nullptr, p, s1, s2);
+    if ((p & 3) == 0) A0[p >> 2] = s1 * scale;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += nt) {
+    float m = -INFINITY;
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A0[i * N + j]);
+    float ssum = 0.f;
+    for (int j = 0; j < N; ++j) {
+      const float e = expf(A0[i * N + j] - m);
+      A0[i * N + j] = e;
+      ssum += e;
+    }
+    const float inv = 1.f / ssum;
+    for (int j = 0; j < N; ++j) A0[i * N + j] *= inv;
+  }
+  commit(sm + L.qc + nd, sm + L.kc + nd, sm + L.vc + nd);  // channel 1 -> buffer 1
+  __syncthreads();
+  for (int p = tid; p < N * dh; p += nt) {
+    const int i = p / dh, d = p - i * dh;
+    float acc = 0.f;
+    for (int j = 0; j < N; ++j) acc = fmaf(A0[i * N + j], v0[j * ld + d], acc);
+    store_o(0, i, d, acc);
+  }
+
+  // ---- channels 1 .. C-1
+  for (int c = 1; c < C; ++c) {
+    const int buf = c & 1;
+    const float* qc = sm + L.qc + buf * nd;
+    const float* kc = sm + L.kc + buf * nd;
+    const float* vc = sm + L.vc + buf * nd;
+    if (c + 1 < C) prefetch(c + 1);
+    const bool tang = c <= T;
+    const int k = c - T - 2;  // flow index (>= 0 for flow channels)
+    // phase A: scores
+    for (int p = tid; p < 4 * nn; p += nt) {
+      float s1, s2;
+      if (tang) {
+        dots(qc, k0, q0, kc, qc, kc, p, s1, s2);
+      } else if (k < 0) {
+        dots(qc, k0, q0, kc, nullptr, nullptr, p, s1, s2);
+      } else {
+        dots(qc, k0, q0, kc, qu + k * nd, ku + k * nd, p, s1, s2);
+      }
+      if ((p & 3) == 0) {
+        const int pair = p >> 2;
+        if (tang) {
+          S[pair] = s1 * scale;
+          P[pair] = s2;
+        } else if (k < 0) {
+          S[pair] = s1 * scale + accS[pair];
+          P[pair] = T2[pair];
+        } else {
+          S[pair] = scale * (s1 + 2.f * s2);
+          const float u = SuB[k * nn + pair];
+          P[pair] = u * u;
+        }
+      }
+    }
+    __syncthreads();
+    // phase B: softmax derivatives
+    for (int p = tid; p < nn; p += nt) {
+      const int i = p / N;
+      if (tang) {
+        const int t = c - 1;
+        float m = 0.f;
+        for (int j = 0; j < N; ++j) m = fmaf(A0[i * N + j], S[i * N + j], m);
+        const float sb = S[p] - m;
+        const float at = A0[p] * sb;
+        accS[p] = fmaf(2.f * scale, P[p], accS[p]);
+        T2[p] = fmaf(sb, sb, T2[p]);
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) {
+          const float a = al[kk * T + t];
+          SuB[kk * nn + p] = fmaf(a, sb, SuB[kk * nn + p]);
+          Au[kk * nn + p] = fmaf(a, at, Au[kk * nn + p]);
+        }
+        Rm[p] = at;
+      } else {
+        float m1 = 0.f, m2 = 0.f;
+        for (int j = 0; j < N; ++j) {
+          m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
+          m2 = fmaf(A0[i * N + j], P[i * N + j], m2);
+        }
+        Rm[p] = A0[p] * ((S[p] - m1) + (P[p] - m2));
+      }
+    }
+    __syncthreads();
+    // phase C: outputs.  Thread (d = lane, g = wave) owns rows i = g + 4r (r < RPT): the
+    // v loads are shared by its rows and the running sums of the flow first-order parts
+    // (qu, ku, vu) and of 2 sum_t A_t v_t stay in registers through the tangent loop.
+    if (d_own < dh) {
+      float acc[RPT], acc2[RPT];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) acc[r] = acc2[r] = 0.f;
+      for (int j = 0; j < N; ++j) {
+        const float v0j = v0[j * ld + d_own], vcj = vc[j * ld + d_own];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+          const int i = g_own + 4 * r;
+          if (i < N) {
+            const float at = Rm[i * N + j];
+            acc[r] = fmaf(at, v0j, fmaf(A0[i * N + j], vcj, acc[r]));
+            acc2[r] = fmaf(at, vcj, acc2[r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const int i = g_own + 4 * r;
+        if (i >= N) continue;
+        const int q = i * ld + d_own;
+        float out = acc[r];
+        if (tang) {
+          const int t = c - 1;
+          rOL[r] = fmaf(2.f, acc2[r], rOL[r]);
+          const float qv = qc[q], kv = kc[q], vv = vc[q];
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk) {
+            const float a = al[kk * T + t];
+            rQu[kk][r] = fmaf(a, qv, rQu[kk][r]);
+            rKu[kk][r] = fmaf(a, kv, rKu[kk][r]);
+            rVu[kk][r] = fmaf(a, vv, rVu[kk][r]);
+          }
+          if (c == T) {  // last tangent: publish the accumulated first-order parts
+            accOL[q] = rOL[r];
+#pragma unroll
+            for (int kk = 0; kk < 3; ++kk) {
+              qu[kk * nd + q] = rQu[kk][r];
+              ku[kk * nd + q] = rKu[kk][r];
+              vu[kk * nd + q] = rVu[kk][r];
+            }
+          }
+        } else if (k < 0) {
+          out += rOL[r];
+        } else {
+          float a2 = 0.f;
+          for (int j = 0; j < N; ++j) a2 = fmaf(Au[k * nn + i * N + j], vu[k * nd + j * ld + d_own], a2);
+          out = fmaf(2.f, a2, out);
+        }
+        store_o(c, i, d_own, out);
+      }
+    }
+    if (c + 1 < C) {
+      const int nb = (c + 1) & 1;
+      commit(sm + L.qc + nb * nd, sm + L.kc + nb * nd, sm + L.vc + nb * nd);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Channel kernel v3 (N <= 8, dh = 64): ONE WAVE per (walker, head), no block barriers.
+// Lane = feature column d for loads / outputs (the running first-order flow sums live in
+// registers), lane = (score pair, quarter of d) for the scores (16-byte LDS reads).
+// LDS is private to the wave; LDS ops of one wave execute in order, so a
+// __builtin_amdgcn_wave_barrier() (compiler ordering) separates the phases.
+template <int N>
+__global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restrict__ qkv,
+                                                            const float* __restrict__ geo, float* __restrict__ o,
+                                                            int H) {
+  constexpr int dh = 64, ld = 68, T = 2 * N, C = 2 * N + 5, nn = N * N;
+  extern __shared__ float sm[];
+  float *q0 = sm, *k0 = q0 + N * ld, *v0 = k0 + N * ld, *qc = v0 + N * ld, *kc = qc + N * ld, *vc = kc + N * ld;
+  float *A0 = vc + N * ld, *S = A0 + nn, *P = S + nn, *Rm = P + nn, *accS = Rm + nn, *T2 = accS + nn;
+  float *SuB = T2 + nn, *Au = SuB + 3 * nn, *QK = Au + 3 * nn, *al = QK + 3 * nn;
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H, lane = threadIdx.x;
+  const int D = H * dh;
+  const float scale = 0.125f;  // 1 / sqrt(64)
+  const float* base = qkv + (size_t)b * N * C * (3 * D) + h * dh + lane;
+  float pq[N], pk[N], pv[N];
+  auto prefetch = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float* r = base + (size_t)(i * C + c) * (3 * D);
+      pq[i] = r[0];
+      pk[i] = r[D];
+      pv[i] = r[2 * D];
+    }
+  };
+  auto commit = [&](float* qd, float* kd, float* vd) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      qd[i * ld + lane] = pq[i];
+      kd[i * ld + lane] = pk[i];
+      vd[i * ld + lane] = pv[i];
+    }
+  };
+  float* obase = o + (size_t)b * N * C * D + h * dh + lane;
+  auto wsync = [] { __builtin_amdgcn_wave_barrier(); };
+  // 4 lanes per pair; dots over 16 columns with float4 LDS reads
+  auto dot16 = [&](const float* x, const float* y) {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 a = *reinterpret_cast<const float4*>(x + 4 * m);
+      const float4 c = *reinterpret_cast<const float4*>(y + 4 * m);
+      s = fmaf(a.x, c.x, fmaf(a.y, c.y, fmaf(a.z, c.z, fmaf(a.w, c.w, s))));
+    }
+    return s;
+  };
+
+  if (lane < T) {
+    const int i = lane >> 1;
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((lane & 1) == 0)
+        a = (k == 0) ? -g.z : (k == 1 ? g.w : 0.f);
+      else
+        a = (k == 0) ? -(g.y * g.w) : (k == 1 ? -(g.y * g.z) : g.x);
+      al[k * T + lane] = a;
+    }
+  }
+  prefetch(0);
+  commit(q0, k0, v0);
+  prefetch(1);
+  for (int p = lane; p < nn; p += 64) {
+    accS[p] = 0.f;
+    T2[p] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) SuB[k * nn + p] = Au[k * nn + p] = 0.f;
+  }
+  wsync();
+  // ---- value channel
+  for (int p = lane; p < 4 * nn; p += 64) {
+    const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
+    float s = dot16(q0 + i * ld + 16 * qt, k0 + j * ld + 16 * qt);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (qt == 0) A0[pair] = s * scale;
+  }
+  wsync();
+  if (lane < N) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A0[lane * N + j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A0[lane * N + j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A0[lane * N + j] = e[j] * inv;
+  }
+  wsync();
+  {
+    float v0r[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) v0r[j] = v0[j * ld + lane];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(A0[i * N + j], v0r[j], acc);
+      obase[(size_t)(i * C) * D] = acc;
+    }
+  }
+  float rOL[N], rQu[3][N], rKu[3][N], rVu[3][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    rOL[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rQu[k][i] = rKu[k][i] = rVu[k][i] = 0.f;
+  }
+
+  for (int c = 1; c < C; ++c) {
+    wsync();
+    commit(qc, kc, vc);
+    if (c + 1 < C) prefetch(c + 1);
+    wsync();
+    const bool tang = c <= T;
+    const int k = c - T - 2;
+    // phase A: scores
+    for (int p = lane; p < 4 * nn; p += 64) {
+      const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
+      const int oi = i * ld + 16 * qt, oj = j * ld + 16 * qt;
+      float s1 = dot16(qc + oi, k0 + oj) + dot16(q0 + oi, kc + oj);
+      float s2 = tang ? dot16(qc + oi, kc + oj) : 0.f;
+      s1 += __shfl_xor(s1, 1, 64);
+      s1 += __shfl_xor(s1, 2, 64);
+      s2 += __shfl_xor(s2, 1, 64);
+      s2 += __shfl_xor(s2, 2, 64);
+      if (qt == 0) {
+        if (tang) {
+          S[pair] = s1 * scale;
+          P[pair] = s2;
+        } else if (k < 0) {
+          S[pair] = s1 * scale + accS[pair];
+          P[pair] = T2[pair];
+        } else {
+          S[pair] = scale * (s1 + 2.f * QK[k * nn + pair]);
+          const float u = SuB[k * nn + pair];
+          P[pair] = u * u;
+        }
+      }
+    }
+    wsync();
+    // phase B: softmax derivatives (lane = pair)
+    for (int p = lane; p < nn; p += 64) {
+      const int i = p / N;
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
+        m2 = fmaf(A0[i * N + j], P[i * N + j], m2);
+      }
+      if (tang) {
+        const int t = c - 1;
+        const float sb = S[p] - m1;
+        const float at = A0[p] * sb;
+        accS[p] = fmaf(2.f * scale, P[p], accS[p]);
+        T2[p] = fmaf(sb, sb, T2[p]);
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) {
+          const float a = al[kk * T + t];
+          SuB[kk * nn + p] = fmaf(a, sb, SuB[kk * nn + p]);
+          Au[kk * nn + p] = fmaf(a, at, Au[kk * nn + p]);
+        }
+        Rm[p] = at;
+      } else {
+        Rm[p] = A0[p] * ((S[p] - m1) + (P[p] - m2));
+      }
+    }
+    wsync();
+    // phase C: outputs (lane = d)
+    {
+      float v0r[N], vcr[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        v0r[j] = v0[j * ld + lane];
+        vcr[j] = vc[j * ld + lane];
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        float acc = 0.f, acc2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const float r = Rm[i * N + j];
+          acc = fmaf(r, v0r[j], fmaf(A0[i * N + j], vcr[j], acc));
+          if (tang) acc2 = fmaf(r, vcr[j], acc2);
+        }
+        if (tang) {
+          const int t = c - 1;
+          rOL[i] = fmaf(2.f, acc2, rOL[i]);
+          const float qv = qc[i * ld + lane], kv = kc[i * ld + lane];
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk) {
+            const float a = al[kk * T + t];
+            rQu[kk][i] = fmaf(a, qv, rQu[kk][i]);
+            rKu[kk][i] = fmaf(a, kv, rKu[kk][i]);
+            rVu[kk][i] = fmaf(a, vcr[i], rVu[kk][i]);
+          }
+        } else if (k < 0) {
+          acc += rOL[i];
+        } else {
+          float a2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            // rVu[k][j] with a runtime k: select without dynamic register indexing
+            const float vu = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
+            a2 = fmaf(Au[k * nn + i * N + j], vu, a2);
+          }
+          acc = fmaf(2.f, a2, acc);
+        }
+        obase[(size_t)(i * C + c) * D] = acc;
+      }
+    }
+    if (c == T) {  // last tangent: qu_k . ku_k^T for the flow channels (wave reductions)
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            const float v = wave_sum(rQu[kk][i] * rKu[kk][j]);
+            if (lane == 0) QK[kk * nn + i * N + j] = v;
+          }
+    }
+  }
+}
+
+template <int N>
+void launch_wave(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s) {
+  const int nn = N * N;
+  const size_t smem = (size_t)(6 * N * 68 + 15 * nn + 6 * N) * sizeof(float);
+  hipLaunchKernelGGL(attention_wave_kernel<N>, dim3(nw * d.H), dim3(64), smem, s, qkv, geo, o, d.H);
+}
+
+template <int PF, int RPT>
+void launch_ch(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s) {
+  const size_t smem = (size_t)attn_layout2(d.N, d.dh).total * sizeof(float);
+  ensure_smem(attention_ch_kernel<PF, RPT>, smem);
+  hipLaunchKernelGGL((attention_ch_kernel<PF, RPT>), dim3(nw * d.H), dim3(256), smem, s, qkv, geo, o, d.N, d.H,
+                     d.dh);
+}
+
 }  // namespace
 
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s) {
+  // channel kernel v2 needs dh <= 64 (one feature column per lane) and dh % 4 == 0;
+  // PF = float4 prefetch slots >= 3 N dh / 1024, RPT = rows per thread >= N / 4
+  if (C > 1 && d.dh == 64 && d.N <= 8) {
+    switch (d.N) {
+      case 1: launch_wave<1>(d, qkv, geo, o, nw, s); return;
+      case 2: launch_wave<2>(d, qkv, geo, o, nw, s); return;
+      case 3: launch_wave<3>(d, qkv, geo, o, nw, s); return;
+      case 4: launch_wave<4>(d, qkv, geo, o, nw, s); return;
+      case 5: launch_wave<5>(d, qkv, geo, o, nw, s); return;
+      case 6: launch_wave<6>(d, qkv, geo, o, nw, s); return;
+      case 7: launch_wave<7>(d, qkv, geo, o, nw, s); return;
+      default: launch_wave<8>(d, qkv, geo, o, nw, s); return;
+    }
+  }
+  if (C > 1 && d.dh % 4 == 0 && d.dh <= 64 && d.N <= 32) {
+    const int N = d.N;
+    if (N <= 4)
+      launch_ch<1, 1>(d, qkv, geo, o, nw, s);
+    else if (N <= 8)
+      launch_ch<2, 2>(d, qkv, geo, o, nw, s);
+    else if (N <= 12)
+      launch_ch<3, 3>(d, qkv, geo, o, nw, s);
+    else if (N <= 16)
+      launch_ch<3, 4>(d, qkv, geo, o, nw, s);
+    else if (N <= 20)
+      launch_ch<4, 5>(d, qkv, geo, o, nw, s);
+    else if (N <= 24)
+      launch_ch<5, 6>(d, qkv, geo, o, nw, s);
+    else
+      launch_ch<6, 8>(d, qkv, geo, o, nw, s);
+    return;
+  }
   const AttnSmem L = attn_layout(d.N, d.dh, d.T, C);
   const size_t smem = (size_t)L.total * sizeof(float);
   const int threads = (C == 1) ? 64 : 256;

@@ -161,7 +161,8 @@ int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream);
  * dh_profile_read fills out[k*4 + {0,1,2,3}] = {launches, total ms, algorithmic
  * FLOPs, algorithmic bytes} for kernel class k (returns the number of classes):
  *   0 GEMM  1 attention  2 LayerNorm  3 input  4 det (log psi)  5 det (energy)
- *   6 MCMC proposal/accept.  Synchronises on the recorded events. */
+ *   6 MCMC proposal/accept; 7-10 = classes 0-3 launched with 2N+5 channels
+ *   (local energy).  Synchronises on the recorded events. */
 int dh_profile_enable(dh_handle* h, int on);
 int dh_profile_read(dh_handle* h, double* out, int reset);
 

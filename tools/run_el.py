@@ -1,0 +1,24 @@
+"""Run the C2 local energy a few times (profiling target for rocprofv3 --pmc)."""
+
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from deephall_amd import config  # noqa: E402
+from deephall_amd.hamiltonian import _run_local_energy  # noqa: E402
+from deephall_amd.networks import make_network  # noqa: E402
+from deephall_amd.random import Key, PRNGKey  # noqa: E402
+from deephall_amd.train import init_guess  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+model = make_network(config.System(nspins=(6, 0), flux=15), config.Network())
+params = model.init(PRNGKey(42), device="cuda")
+x = init_guess(Key(1), B, 6, "cuda", network=model)
+for _ in range(reps):
+    _run_local_energy(model, params, x)
+torch.cuda.synchronize()
+print("done")
