@@ -185,6 +185,7 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
   sizes.push_back((size_t)D * d.ld_orb);
   sizes.push_back((size_t)d.ld_orb);
   sizes.push_back(2);
+  sizes.push_back((size_t)4 * 3 * D);  // W0 @ Wqkv of layer 0 (folded input projection)
   size_t off = 0;
   for (size_t s : sizes) {
     h->offsets.push_back(off);
@@ -248,6 +249,7 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
   h->p.Worb = P + h->offsets[s++];
   h->p.borb = P + h->offsets[s++];
   h->p.jastrow = P + h->offsets[s++];
+  h->p.W0qkv = P + h->offsets[s++];
   h->params_set = true;
   return DH_OK;
 }
@@ -274,12 +276,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
   };
   {
-    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD, f4 * R * DD);
-    launch_input(d, x, P.W0, w.h, w.geo, nw, C, s);
+    const bool fold = d.L > 0;  // layer-1 q|k|v straight from the features (K = 4)
+    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (fold ? 4 : 1), f4 * R * DD * (fold ? 4 : 1));
+    launch_input(d, x, P.W0, fold ? P.W0qkv : nullptr, fold ? P.layer[0].bqkv : nullptr, w.h, fold ? w.qkv : nullptr,
+                 w.geo, nw, C, s);
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    if (l > 0) gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 4.0 * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);

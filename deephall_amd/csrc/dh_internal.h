@@ -31,6 +31,7 @@ struct Params {
   const float* W0;
   LayerParams layer[16];
   const float *Worb, *borb, *jastrow;
+  const float* W0qkv;  // [4][3D] = W0 @ Wqkv of layer 0 (folded on the host)
 };
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
@@ -63,8 +64,10 @@ void set_gemm_variant(int v);
 // input.hip
 // Features (psiformer.py:51-60) of every channel times W0 -> h [rows][D]; also
 // writes geo[nw][N][4] = (sin th, cos th, sin ph, cos ph).
-void launch_input(const Dims& d, const float* x, const float* W0, float* h, float* geo, int nw, int C,
-                  hipStream_t s);
+// With W0qkv != nullptr it also writes layer 1's q|k|v = f (W0 Wqkv) (+ bqkv on value
+// rows): the first attention projection is folded into the K=4 input map.
+void launch_input(const Dims& d, const float* x, const float* W0, const float* W0qkv, const float* bqkv, float* h,
+                  float* qkv, float* geo, int nw, int C, hipStream_t s);
 // Proposal (mcmc.py:67-102): x2 = sph_sampling(x, noise).
 void launch_propose(const Dims& d, const float* x, float* x2, int nw, float width, uint64_t seed, uint64_t step,
                     int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s);

@@ -1,4 +1,7 @@
-// Input layer: electron features of every channel times W0 (psiformer.py:42,51-60).
+// Input layer: electron features of every channel times W0 (psiformer.py:42,51-60),
+// and — folded — layer 1's attention projections q|k|v = f (W0 Wqkv) + b (the
+// product of two linear maps with nothing in between; W0 Wqkv is formed on the host
+// in float64).  This replaces the first K=256 GEMM by a K=4 streaming kernel.
 //
 // Channel c of row (walker b, electron i):
 //   c = 0        [cos th, sin th cos ph, sin th sin ph, s_i]                 (value)
@@ -15,74 +18,89 @@
 namespace dh {
 namespace {
 
-__global__ void input_kernel(const float* __restrict__ x, const float* __restrict__ W0, float* __restrict__ h,
-                             float* __restrict__ geo, int nw, int N, int n_up, int C, int D) {
-  const int D4 = D >> 2;
-  const long total = (long)nw * N * C * D4;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int d4 = idx % D4;
-    const long row = idx / D4;
+constexpr int kRows = 32;  // rows per workgroup
+
+__global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x, const float* __restrict__ W0,
+                                                    const float* __restrict__ W0qkv,
+                                                    const float* __restrict__ bqkv, float* __restrict__ h,
+                                                    float* __restrict__ qkv, float* __restrict__ geo, int rows,
+                                                    int N, int n_up, int C, int D) {
+  extern __shared__ float4 smem4[];
+  const int E = qkv ? 4 * D : D;  // output columns per row (h, then q|k|v)
+  float4* Ws = smem4;             // [4][E/4]: W0 rows then W0qkv rows, per input feature
+  float4* F = Ws + E;             // [kRows] features
+  const int tid = threadIdx.x;
+  const int E4 = E / 4, D4 = D / 4;
+  for (int q = tid; q < 4 * E4; q += blockDim.x) {
+    const int k = q / E4, c4 = q - k * E4;
+    Ws[q] = (c4 < D4) ? reinterpret_cast<const float4*>(W0 + (size_t)k * D)[c4]
+                      : reinterpret_cast<const float4*>(W0qkv + (size_t)k * 3 * D)[c4 - D4];
+  }
+  const int row0 = blockIdx.x * kRows;
+  if (tid < kRows && row0 + tid < rows) {
+    const int row = row0 + tid;
     const int c = row % C;
-    const long e = row / C;  // walker*N + electron
+    const int e = row / C;  // walker*N + electron
     const int i = e % N;
     const float th = x[2 * e], ph = x[2 * e + 1];
     float st, ct, sp, cp;
     sincosf(th, &st, &ct);
     sincosf(ph, &sp, &cp);
     const float rx = st * cp, ry = st * sp, rz = ct;
-    float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
     const int T = 2 * N;
     if (c == 0) {
-      f0 = rz;
-      f1 = rx;
-      f2 = ry;
-      f3 = (i < n_up) ? 1.f : -1.f;
-      if (d4 == 0) {
-        float4 g = make_float4(st, ct, sp, cp);
-        *reinterpret_cast<float4*>(geo + 4 * e) = g;
-      }
+      f = make_float4(rz, rx, ry, (i < n_up) ? 1.f : -1.f);
+      *reinterpret_cast<float4*>(geo + 4 * (size_t)e) = make_float4(st, ct, sp, cp);
     } else if (c <= T) {
       const int t = c - 1;
-      if ((t >> 1) == i) {
-        if ((t & 1) == 0) {
-          f0 = -st;
-          f1 = ct * cp;
-          f2 = ct * sp;
-        } else {
-          f1 = -sp;
-          f2 = cp;
-        }
-      }
+      if ((t >> 1) == i) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
     } else if (c == T + 1) {
-      f0 = -2.f * rz;
-      f1 = -2.f * rx;
-      f2 = -2.f * ry;
+      f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
     } else {
       const int k = c - T - 2;  // 0:x 1:y 2:z
-      f0 = (k == 2) ? 0.f : -rz;
-      f1 = (k == 0) ? 0.f : -rx;
-      f2 = (k == 1) ? 0.f : -ry;
+      f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
     }
-    const float4 w0 = reinterpret_cast<const float4*>(W0)[d4];
-    const float4 w1 = reinterpret_cast<const float4*>(W0 + D)[d4];
-    const float4 w2 = reinterpret_cast<const float4*>(W0 + 2 * D)[d4];
-    const float4 w3 = reinterpret_cast<const float4*>(W0 + 3 * D)[d4];
+    F[tid] = f;
+  }
+  __syncthreads();
+  const int nr = min(kRows, rows - row0);
+  for (int q = tid; q < nr * E4; q += blockDim.x) {
+    const int r = q / E4, c4 = q - r * E4;
+    const float4 f = F[r];
+    const float4 w0 = Ws[c4], w1 = Ws[E4 + c4], w2 = Ws[2 * E4 + c4], w3 = Ws[3 * E4 + c4];
     float4 o;
-    o.x = f0 * w0.x + f1 * w1.x + f2 * w2.x + f3 * w3.x;
-    o.y = f0 * w0.y + f1 * w1.y + f2 * w2.y + f3 * w3.y;
-    o.z = f0 * w0.z + f1 * w1.z + f2 * w2.z + f3 * w3.z;
-    o.w = f0 * w0.w + f1 * w1.w + f2 * w2.w + f3 * w3.w;
-    reinterpret_cast<float4*>(h + row * D)[d4] = o;
+    o.x = f.x * w0.x + f.y * w1.x + f.z * w2.x + f.w * w3.x;
+    o.y = f.x * w0.y + f.y * w1.y + f.z * w2.y + f.w * w3.y;
+    o.z = f.x * w0.z + f.y * w1.z + f.z * w2.z + f.w * w3.z;
+    o.w = f.x * w0.w + f.y * w1.w + f.z * w2.w + f.w * w3.w;
+    const size_t row = (size_t)(row0 + r);
+    if (c4 < D4) {
+      reinterpret_cast<float4*>(h + row * D)[c4] = o;
+    } else {
+      const int q4 = c4 - D4;
+      if (row % C == 0) {
+        const float4 bb = reinterpret_cast<const float4*>(bqkv)[q4];
+        o.x += bb.x;
+        o.y += bb.y;
+        o.z += bb.z;
+        o.w += bb.w;
+      }
+      reinterpret_cast<float4*>(qkv + row * 3 * D)[q4] = o;
+    }
   }
 }
 
 }  // namespace
 
-void launch_input(const Dims& d, const float* x, const float* W0, float* h, float* geo, int nw, int C,
-                  hipStream_t s) {
-  const long total = (long)nw * d.N * C * (d.D / 4);
-  int blocks = (int)std::min<long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(input_kernel, dim3(blocks), dim3(256), 0, s, x, W0, h, geo, nw, d.N, d.n_up, C, d.D);
+void launch_input(const Dims& d, const float* x, const float* W0, const float* W0qkv, const float* bqkv, float* h,
+                  float* qkv, float* geo, int nw, int C, hipStream_t s) {
+  const int rows = nw * d.N * C;
+  const int E = qkv ? 4 * d.D : d.D;
+  const size_t smem = (size_t)(4 * E / 4 + kRows) * sizeof(float4);
+  ensure_smem(input_kernel, smem);
+  hipLaunchKernelGGL(input_kernel, dim3((rows + kRows - 1) / kRows), dim3(256), smem, s, x, W0, W0qkv, bqkv, h, qkv,
+                     geo, rows, d.N, d.n_up, C, d.D);
 }
 
 }  // namespace dh

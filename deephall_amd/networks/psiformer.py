@@ -258,6 +258,13 @@ def pack_params(spec: NetworkSpec, params: dict, offsets: list, device) -> torch
             device=dev,
         )
     )
+    # layer-1 q|k|v projection folded into the input map: W0 @ Wqkv (float64), [4][3D]
+    if spec.num_layers > 0:
+        mha = p + "MultiHeadAttention_0/"
+        wq0 = torch.cat([f64(mha + n + "/kernel").reshape(D, D) for n in ("query", "key", "value")], 1)
+        put(f64(p + "Dense_0/kernel") @ wq0)
+    else:
+        seg += 1
     assert seg == len(offsets) - 1
     return buf
 

@@ -94,7 +94,9 @@ const char* dh_version(void);
  *                              zero padded to ld_orb (multiple of 128)
  *   2+8L     borb [ld_orb]
  *   3+8L     jastrow [2]       ee_par, ee_anti
- * Returns the number of segments (4+8L) and writes up to `n` offsets; the
+ *   4+8L     W0qkv [4][3D]     W0 @ Wqkv of layer 0: the first attention projection
+ *                              folded into the K=4 input map (unused if L == 0)
+ * Returns the number of segments (5+8L) and writes up to `n` offsets; the
  * total float count is offsets[nseg] (written if n > nseg). */
 int dh_param_layout(const dh_handle* h, size_t* offsets, int n);
 /* Copy the packed parameter buffer (device pointer, `count` floats) into the

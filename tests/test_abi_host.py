@@ -49,7 +49,7 @@ def test_create_layout_workspace():
     lib, spec, h, rc = make_handle()
     assert rc == 0
     nseg = lib.dh_param_layout(h, None, 0)
-    assert nseg == 4 + 8 * spec.num_layers
+    assert nseg == 5 + 8 * spec.num_layers
     offs = (C.c_size_t * (nseg + 1))()
     lib.dh_param_layout(h, offs, nseg + 1)
     offs = list(offs)
@@ -108,6 +108,9 @@ def test_pack_params_layout_matches_reference_tree():
     assert torch.allclose(worb[:, 3 * MNK : 4 * MNK], p[ob + "DenseGeneral_3/kernel"].double().reshape(D, MNK))
     jas = buf[offs[3 + 8 * L] : offs[3 + 8 * L] + 2]
     assert jas.tolist() == [1.0, 1.0]
+    w0qkv = buf[offs[4 + 8 * L] : offs[4 + 8 * L] + 4 * 3 * D].reshape(4, 3 * D)
+    wq0 = torch.cat([p[mha + n + "/kernel"].double().reshape(D, D) for n in ("query", "key", "value")], 1)
+    assert torch.allclose(w0qkv, p["PsiformerLayers_0/Dense_0/kernel"].double() @ wq0, atol=1e-6)
     lib.dh_destroy(h)
 
 
