@@ -192,11 +192,37 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
   int* piv = reinterpret_cast<int*>(logdet + 1);
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const FView F{Fp, ldF, M, N, K};
+  float* cart = reinterpret_cast<float*>(piv + 2);  // [N][3] unit vectors
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
     E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
   }
+  for (int i = tid; i < N; i += nt) {
+    float st, ct, sp, cp;
+    sincosf(x[2 * (b * N + i)], &st, &ct);
+    sincosf(x[2 * (b * N + i) + 1], &sp, &cp);
+    cart[3 * i] = st * cp;
+    cart[3 * i + 1] = st * sp;
+    cart[3 * i + 2] = ct;
+  }
   __syncthreads();
+  // Jastrow (blocks.py:76-121): chord distances on the unit sphere, pairs spread over the
+  // wave, accumulated in double and reduced with shuffles (one 64-lane wave per walker)
+  double Jw = 0.0;
+  {
+    const double ap = jas[0], aa = jas[1];
+    for (int q = tid; q < N * N; q += nt) {
+      const int i = q / N, j = q - (q / N) * N;
+      if (j <= i) continue;
+      const double dx = (double)cart[3 * j] - cart[3 * i], dy = (double)cart[3 * j + 1] - cart[3 * i + 1],
+                   dz = (double)cart[3 * j + 2] - cart[3 * i + 2];
+      const double r = sqrt(dx * dx + dy * dy + dz * dz);
+      const bool same = (i < n_up) == (j < n_up);
+      double f1, f2;
+      Jw += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+    }
+    for (int o = 32; o > 0; o >>= 1) Jw += __shfl_xor(Jw, o, 64);
+  }
   for (int k = 0; k < K; ++k) {
     for (int idx = tid; idx < N * N; idx += nt) {
       const int i = idx / N, j = idx % N;
@@ -223,22 +249,7 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
     }
     float val_re = 0.5f * logf(zr * zr + zi * zi) + lmax;
     float val_im = atan2f(zi, zr);
-    // Jastrow (blocks.py:76-121), chord distance on the unit sphere
-    double J = 0.0;
-    const double ap = jas[0], aa = jas[1];
-    for (int i = 0; i < N; ++i) {
-      const float ti = x[2 * (b * N + i)], pi_ = x[2 * (b * N + i) + 1];
-      const double xi = sin(ti) * cos(pi_), yi = sin(ti) * sin(pi_), zi_ = cos(ti);
-      for (int j = i + 1; j < N; ++j) {
-        const float tj = x[2 * (b * N + j)], pj = x[2 * (b * N + j) + 1];
-        const double dx = sin(tj) * cos(pj) - xi, dy = sin(tj) * sin(pj) - yi, dz = cos(tj) - zi_;
-        const double r = sqrt(dx * dx + dy * dy + dz * dz);
-        const bool same = (i < n_up) == (j < n_up);
-        double f1, f2;
-        J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
-      }
-    }
-    logpsi[2 * b] = val_re + (float)J;
+    logpsi[2 * b] = val_re + (float)Jw;
     logpsi[2 * b + 1] = val_im;
   }
 }
@@ -696,7 +707,7 @@ void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStrea
 
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s) {
-  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4) * sizeof(float);
+  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 3 * d.N) * sizeof(float);
   hipLaunchKernelGGL(det_value_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N,
                      d.n_up, d.M, d.K);
 }
