@@ -241,10 +241,159 @@ __global__ __launch_bounds__(256) void layernorm_value_kernel(const float* X, co
   }
 }
 
+// Channel rows, N <= 8, D = 256: ONE WAVE per (walker, electron).  Lane l owns columns
+// 4l..4l+3 of all C = 2N+5 channel rows in registers; every mean over D is a wave
+// reduction — no LDS, no barriers.  Same algebra as layernorm_kernel.
+template <int N>
+__global__ __launch_bounds__(256) void layernorm_ch_wave_kernel(const float* X, const float* __restrict__ Z,
+                                                                const float* __restrict__ ln,
+                                                                const float* __restrict__ geo, float* h, int ne,
+                                                                int mode) {
+  constexpr int T = 2 * N, C = 2 * N + 5, D = 256;
+  const int e = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // walker*N + electron
+  if (e >= ne) return;
+  const int lane = threadIdx.x & 63;
+  const int b = e / N;
+  // flow coefficients alpha[k][t] (uniform over the wave)
+  float al[3][T];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    al[0][2 * i] = -g.z;
+    al[1][2 * i] = g.w;
+    al[2][2 * i] = 0.f;
+    al[0][2 * i + 1] = -(g.y * g.w);
+    al[1][2 * i + 1] = -(g.y * g.z);
+    al[2][2 * i + 1] = g.x;
+  }
+  const size_t r4 = (size_t)e * C * (D / 4) + lane;  // float4 index of (row e*C, column quad lane)
+  float4 z[C];
+  if (mode == 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) z[c] = reinterpret_cast<const float4*>(X)[r4 + c * (D / 4)];
+  } else {
+    float4 zz[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      zz[c] = reinterpret_cast<const float4*>(Z)[r4 + c * (D / 4)];
+      z[c] = reinterpret_cast<const float4*>(h)[r4 + c * (D / 4)];
+    }
+    // y = h + tanh_ch(Z), componentwise
+#define DH_TANH_COMP(F)                                                         \
+  {                                                                             \
+    const float y0 = tanhf(zz[0].F);                                            \
+    const float d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;                        \
+    float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;                               \
+    _Pragma("unroll") for (int t = 0; t < T; ++t) {                             \
+      const float zt = zz[1 + t].F;                                             \
+      sq = fmaf(zt, zt, sq);                                                    \
+      u0 = fmaf(al[0][t], zt, u0);                                              \
+      u1 = fmaf(al[1][t], zt, u1);                                              \
+      u2 = fmaf(al[2][t], zt, u2);                                              \
+      z[1 + t].F += d1 * zt;                                                    \
+    }                                                                           \
+    z[0].F += y0;                                                               \
+    z[1 + T].F += d1 * zz[1 + T].F + d2 * sq;                                   \
+    z[2 + T].F += d1 * zz[2 + T].F + d2 * u0 * u0;                              \
+    z[3 + T].F += d1 * zz[3 + T].F + d2 * u1 * u1;                              \
+    z[4 + T].F += d1 * zz[4 + T].F + d2 * u2 * u2;                              \
+  }
+    DH_TANH_COMP(x) DH_TANH_COMP(y) DH_TANH_COMP(z) DH_TANH_COMP(w)
+#undef DH_TANH_COMP
+  }
+  // channel means, centre
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float mu = wave_sum((z[c].x + z[c].y) + (z[c].z + z[c].w)) * (1.f / D);
+    z[c].x -= mu;
+    z[c].y -= mu;
+    z[c].z -= mu;
+    z[c].w -= mu;
+  }
+  float4 u[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    u[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      u[k].x = fmaf(al[k][t], z[1 + t].x, u[k].x);
+      u[k].y = fmaf(al[k][t], z[1 + t].y, u[k].y);
+      u[k].z = fmaf(al[k][t], z[1 + t].z, u[k].z);
+      u[k].w = fmaf(al[k][t], z[1 + t].w, u[k].w);
+    }
+  }
+  auto dot4 = [](const float4& a, const float4& b) { return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w); };
+  float p[C], q[T], uu[3];
+#pragma unroll
+  for (int c = 0; c < C; ++c) p[c] = wave_sum(dot4(z[0], z[c])) * (1.f / D);
+#pragma unroll
+  for (int t = 0; t < T; ++t) q[t] = wave_sum(dot4(z[1 + t], z[1 + t])) * (1.f / D);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) uu[k] = wave_sum(dot4(u[k], u[k])) * (1.f / D);
+  const float s = 1.f / sqrtf(p[0] + 1e-5f), s2 = s * s;
+  float at[T], cl = 0.f;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    at[t] = s2 * p[1 + t];
+    cl += 3.f * at[t] * at[t] - s2 * q[t];
+  }
+  float au[3], cs[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    au[k] = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) au[k] = fmaf(al[k][t], at[t], au[k]);
+    cs[k] = 3.f * au[k] * au[k] - s2 * uu[k];
+  }
+  const float4 g = reinterpret_cast<const float4*>(ln)[lane];
+  const float4 bb = reinterpret_cast<const float4*>(ln + D)[lane];
+  float4* out = reinterpret_cast<float4*>(h) + r4;
+  const float aL = s2 * p[1 + T];
+#define DH_LN_OUT(F)                                                                             \
+  {                                                                                              \
+    const float z0 = z[0].F, gs = g.F * s;                                                       \
+    float sat = 0.f;                                                                             \
+    _Pragma("unroll") for (int t = 0; t < T; ++t) sat = fmaf(at[t], z[1 + t].F, sat);            \
+    o0.F = g.F * (s * z0) + bb.F;                                                                \
+    _Pragma("unroll") for (int t = 0; t < T; ++t) ot[t].F = gs * (z[1 + t].F - at[t] * z0);      \
+    oL.F = gs * (z[1 + T].F - aL * z0 - 2.f * sat + cl * z0);                                    \
+    _Pragma("unroll") for (int k = 0; k < 3; ++k) oS[k].F =                                      \
+        gs * (z[2 + T + k].F - s2 * p[2 + T + k] * z0 - 2.f * au[k] * u[k].F + cs[k] * z0);     \
+  }
+  float4 o0, ot[T], oL, oS[3];
+  DH_LN_OUT(x) DH_LN_OUT(y) DH_LN_OUT(z) DH_LN_OUT(w)
+#undef DH_LN_OUT
+  out[0] = o0;
+#pragma unroll
+  for (int t = 0; t < T; ++t) out[(1 + t) * (D / 4)] = ot[t];
+  out[(1 + T) * (D / 4)] = oL;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[(2 + T + k) * (D / 4)] = oS[k];
+}
+
+template <int N>
+void launch_ln_wave(const float* X, const float* Z, const float* ln, const float* geo, float* h, int ne, int mode,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(layernorm_ch_wave_kernel<N>, dim3((ne + 3) / 4), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode);
+}
+
 }  // namespace
 
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
                       int nw, int C, int mode, hipStream_t s) {
+  if (C > 1 && d.D == 256 && d.N <= 8) {
+    const int ne = nw * d.N;
+    switch (d.N) {
+      case 1: launch_ln_wave<1>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 2: launch_ln_wave<2>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 3: launch_ln_wave<3>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 4: launch_ln_wave<4>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 5: launch_ln_wave<5>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 6: launch_ln_wave<6>(X, Z, ln, geo, h, ne, mode, s); return;
+      case 7: launch_ln_wave<7>(X, Z, ln, geo, h, ne, mode, s); return;
+      default: launch_ln_wave<8>(X, Z, ln, geo, h, ne, mode, s); return;
+    }
+  }
   if (C == 1 && (d.D == 256 || d.D == 512)) {
     const int rows = nw * d.N;
     if (d.D == 256)
