@@ -153,13 +153,13 @@ def main():
                 "ms_per_step": ms / args.steps,
                 "avg_us": 1e3 * ms / cnt,
             }
-    # dominant kernel: gemm_f32_kernel, all its launches in the timed region (log-psi and
+    # dominant kernel: gemm_nt_kernel, all its launches in the timed region (log-psi and
     # local-energy GEMMs; classes 0 and 7 of dh_profile_read)
     ig = kinds.index("gemm_ch")
     g_cnt, g_ms, g_fl, g_by = (prof[q] + prof[4 * ig + q] for q in range(4))
     achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
     roofline = {
-        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)",
+        "kernel": "gemm_nt_kernel (LDS-DMA staged, v_mfma_f32_32x32x2_f32)",
         "bound": "mfma",
         "achieved": round(achieved, 2),
         "peak": PEAK_F32_MFMA_TFLOPS,

@@ -92,10 +92,11 @@ struct Profiler {
 struct dh_handle {
   dh_config cfg;
   Dims d;
-  Params p;
+  Params p{};
   std::vector<size_t> offsets;  // nseg + 1
   float* params = nullptr;
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
+  float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
   std::vector<float> norm_host;
   bool params_set = false;
   Profiler prof;
@@ -212,6 +213,7 @@ void dh_destroy(dh_handle* h) {
   }
   if (h->params) (void)hipFree(h->params);
   if (h->norm) (void)hipFree(h->norm);
+  if (h->wt) (void)hipFree(h->wt);
   delete h;
 }
 
@@ -250,6 +252,33 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
   h->p.borb = P + h->offsets[s++];
   h->p.jastrow = P + h->offsets[s++];
   h->p.W0qkv = P + h->offsets[s++];
+  // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
+  // NT GEMM kernels whose LDS-DMA staging wants k contiguous in both operands.
+  if (d.D % 32 == 0) {
+    const int D = d.D;
+    const size_t sq = (size_t)round_up(D, kRowPad) * D, sqkv = (size_t)round_up(3 * D, kRowPad) * D;
+    const size_t sorb = (size_t)round_up(d.orb_cols, kRowPad) * D;
+    const size_t total = (size_t)d.L * (sqkv + 2 * sq) + sorb;
+    if (!h->wt) HIP_TRY(hipMalloc(&h->wt, total * sizeof(float)));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(h->wt, 0, total * sizeof(float), st));
+    float* q = h->wt;
+    for (int l = 0; l < d.L; ++l) {
+      LayerParams& lp = h->p.layer[l];
+      launch_transpose(lp.Wqkv, 3 * D, D, 3 * D, q, D, st);
+      lp.WqkvT = q;
+      q += sqkv;
+      launch_transpose(lp.Wol, D, D, D, q, D, st);
+      lp.WolT = q;
+      q += sq;
+      launch_transpose(lp.Wm, D, D, D, q, D, st);
+      lp.WmT = q;
+      q += sq;
+    }
+    launch_transpose(h->p.Worb, d.ld_orb, D, d.orb_cols, q, D, st);
+    h->p.WorbT = q;
+    HIP_TRY(hipGetLastError());
+  }
   h->params_set = true;
   return DH_OK;
 }
@@ -270,10 +299,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const int rows = nw * d.N * C;
   const int D = d.D;
   const double R = rows, DD = D, f4 = 4.0;
-  auto gemm = [&](const float* X, int ldx, const float* W, int ldw, const float* bias, const float* Res, int ldr,
-                  float* Y, int ldy, int ncols, int K) {
+  const bool nt = P.WorbT != nullptr;
+  auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, int ldw, const float* bias,
+                  const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
     PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
-    launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
+    if (nt)
+      launch_gemm_nt(X, ldx, Wt, K, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
+    else
+      launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
   };
   {
     const bool fold = d.L > 0;  // layer-1 q|k|v straight from the features (K = 4)
@@ -283,24 +316,24 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0) gemm(w.h, D, lp.Wqkv, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    if (l > 0) gemm(w.h, D, lp.Wqkv, lp.WqkvT, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 4.0 * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
-    gemm(w.o, D, lp.Wol, D, lp.bol, w.h, D, w.t, D, D, D);
+    gemm(w.o, D, lp.Wol, lp.WolT, D, lp.bol, w.h, D, w.t, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
       launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
     }
-    gemm(w.h, D, lp.Wm, D, lp.bm, nullptr, 0, w.o, D, D, D);
+    gemm(w.h, D, lp.Wm, lp.WmT, D, lp.bm, nullptr, 0, w.o, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 3.0 * DD);
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  gemm(w.h, D, P.Worb, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
+  gemm(w.h, D, P.Worb, P.WorbT, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
 
@@ -420,8 +453,14 @@ size_t dh_debug_f_offset(const dh_handle* h, int B, int op) {
 // Test hook: one GEMM launch of kernel variant `variant` (-1 = default).
 int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
                   int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream) {
-  launch_gemm_variant(variant < 0 ? 0 : variant, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
-                      (hipStream_t)stream);
+  if (variant >= 100) {
+    if (K % 32 != 0) return fail(DH_EINVAL, "NT GEMM needs K % 32 == 0");
+    launch_gemm_nt_variant(variant - 100, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
+                           (hipStream_t)stream);
+  } else {
+    launch_gemm_variant(variant < 0 ? 0 : variant, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
+                        (hipStream_t)stream);
+  }
   return check_launch();
 }
 

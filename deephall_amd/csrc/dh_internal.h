@@ -26,12 +26,14 @@ struct Dims {
 // Device pointers into the packed parameter buffer.
 struct LayerParams {
   const float *Wqkv, *bqkv, *Wol, *bol, *ln1, *Wm, *bm, *ln2;
+  const float *WqkvT, *WolT, *WmT;  // transposed copies [ncols pad 256][D] for the NT GEMM
 };
 struct Params {
   const float* W0;
   LayerParams layer[16];
   const float *Worb, *borb, *jastrow;
   const float* W0qkv;  // [4][3D] = W0 @ Wqkv of layer 0 (folded on the host)
+  const float* WorbT;  // [orb_cols pad 256][D]
 };
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
@@ -59,7 +61,16 @@ void launch_gemm(const float* X, int ldx, const float* W, int ldw, const float* 
                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
 void launch_gemm_variant(int v, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
                          int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+// NT form: Y = X Wt^T, Wt[n][k] (row stride ldw), K % 32 == 0, Wt rows padded to 256.
+void launch_gemm_nt_variant(int v, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
+                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
+                            hipStream_t s);
 void set_gemm_variant(int v);
+// NT GEMM with the tile shape chosen from (rows, ncols, residual): Wt[n][k], row stride ldw.
+void launch_gemm_nt(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* R, int ldr,
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+// dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).
+void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s);
 
 // input.hip
 // Features (psiformer.py:51-60) of every channel times W0 -> h [rows][D]; also

@@ -166,6 +166,176 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(
   }
 }
 
+// ---- NT form: Y = X Wt^T with the weight stored transposed, Wt[n][k] --------------------
+// Both operands are row-major with k contiguous, so both tiles are staged by
+// global_load_lds_dwordx4 (LDS-DMA: no staging VGPRs, no ds_write) into one LDS image of
+// BK = 32 floats (128 B) per row, 16-B slots XOR-swizzled by (row >> 1) & 7 on the SOURCE
+// address (the DMA destination is lane-linear).  Fragments are read with ds_read_b128:
+// lane (l32, lh) of a 32-row sub-tile takes k = 8g + 4lh + j, j = 0..3, for four
+// consecutive MFMA k-steps (the same bijective k labelling on A and B, so the contraction
+// is exact; only the f32 summation order differs from a k-ordered chain).  Conflict-free:
+// each ds_read_b128 lane group reads 16 distinct rows mod 16 -> 16 distinct slots.
+// Requirements (checked by the launcher): K % 32 == 0; X has round_up(rows, BM) readable
+// rows; Wt has round_up(ncols, BN) readable rows.
+constexpr int NT_BK = 32;
+
+template <int BM, int BN, int WM, int WN, bool HAS_R>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_nt_kernel(
+    const float* __restrict__ X, int ldx, const float* __restrict__ Wt, int ldw, const float* __restrict__ bias,
+    const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, int ntm, int ntn) {
+  constexpr int NWN = BN / WN, NW = (BM / WM) * NWN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int BK = NT_BK, STAGE = (BM + BN) * BK;  // floats per LDS stage
+  constexpr int IA = BM / 8, IB = BN / 8;            // DMA wave-instructions per tile (8 rows each)
+  static_assert(BK == 32, "slot swizzle assumes 8 slots of 16 B per row");
+  extern __shared__ float4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / NWN, wn = wid % NWN;
+
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  // per-lane DMA source for an 8-row group: row = L / 8, logical slot = (L % 8) ^ ((row >> 1) & 7)
+  const int lr = lane >> 3;
+  auto src_slot = [&](int r) { return ((lane & 7) ^ ((r >> 1) & 7)) * 4; };
+  static_assert((IA + IB) % NW == 0, "DMA instructions must divide evenly over the waves");
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) float*)smem);
+  auto stage = [&](int k0, int buf) {
+#pragma unroll
+    for (int t = 0; t < (IA + IB) / NW; ++t) {
+      const int j = wid + t * NW;  // wave-uniform
+      const bool isA = j < IA;
+      const int rg = (isA ? j : j - IA) * 8;  // first row of the 8-row group
+      const int r = rg + lr;
+      const float* src = isA ? X + (size_t)(row0 + r) * ldx + k0 + src_slot(r)
+                             : Wt + (size_t)(col0 + r) * ldw + k0 + src_slot(r);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          lds0 + 4u * (uint32_t)(buf * STAGE + (isA ? 0 : BM * BK) + rg * BK));
+      // LDS-DMA in inline asm: hipcc neither counts it nor inserts a vmcnt(0) before the
+      // next ds_read of the OTHER buffer; completion is waited for explicitly below.
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int nk = K / BK;
+  float rres[TM][TN][16];
+  stage(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) stage((kt + 1) * BK, cur ^ 1);
+    if (HAS_R && kt + 1 == nk) {  // residual loads overlap the last k-tile's MFMAs
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          const int c = col0 + wn * WN + ni * 32 + l32;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int r = row0 + wm * WM + mi * 32 + 4 * lh + (e & 3) + 8 * (e >> 2);
+            rres[mi][ni][e] = (c < ncols && r < rows) ? R[(size_t)r * ldr + c] : 0.f;
+          }
+        }
+    }
+    const float* As = smem + cur * STAGE;
+    const float* Bs = As + BM * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int s = 2 * g + lh;
+      float4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = wm * WM + i * 32 + l32;
+        a[i] = *reinterpret_cast<const float4*>(As + m * BK + ((s ^ ((m >> 1) & 7)) * 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = wn * WN + i * 32 + l32;
+        b[i] = *reinterpret_cast<const float4*>(Bs + n * BK + ((s ^ ((n >> 1) & 7)) * 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int rbase = row0 + wm * WM + mi * 32 + 4 * lh;
+    const int rm0 = (C == 1) ? 0 : rbase % C;
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int c = col0 + wn * WN + ni * 32 + l32;
+      if (c >= ncols) continue;
+      const float bv = bias ? bias[c] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int off = (e & 3) + 8 * (e >> 2);
+        const int r = rbase + off;
+        if (r >= rows) continue;
+        float v = acc[mi][ni][e];
+        if (bias) {
+          bool val = true;
+          if (C > 1) {
+            int t = rm0 + off;
+            while (t >= C) t -= C;
+            val = (t == 0);
+          }
+          if (val) v += bv;
+        }
+        if (HAS_R) v += rres[mi][ni][e];
+        Y[(size_t)r * ldy + c] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_nt(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* R, int ldr,
+               float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  const size_t smem = 2ull * (BM + BN) * NT_BK * sizeof(float);
+  if (R) {
+    ensure_smem(gemm_nt_kernel<BM, BN, WM, WN, true>, smem);
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, true>), dim3(ntm * ntn), dim3(NT), smem, s, X, ldx, Wt, ldw,
+                       bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+  } else {
+    ensure_smem(gemm_nt_kernel<BM, BN, WM, WN, false>, smem);
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false>), dim3(ntm * ntn), dim3(NT), smem, s, X, ldx, Wt, ldw,
+                       bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN>
 void launch_t(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R, int ldr, float* Y,
               int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
@@ -220,7 +390,77 @@ void launch_gemm_variant(int v, const float* X, int ldx, const float* W, int ldw
   }
 }
 
+// NT variants (Wt[n][k]); K % 32 == 0, Wt rows padded to a multiple of 256.
+void launch_gemm_nt_variant(int v, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
+                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
+                            hipStream_t s) {
+  switch (v) {
+    case 1:
+      launch_nt<128, 64, 64, 32>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 2:
+      launch_nt<256, 128, 64, 64>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 3:
+      launch_nt<128, 256, 64, 64>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 4:
+      launch_nt<64, 128, 32, 64>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 5:
+      launch_nt<256, 64, 64, 32>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 6:
+      launch_nt<128, 128, 32, 64>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 7:
+      launch_nt<64, 64, 32, 32>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    default:
+      launch_nt<128, 128, 64, 64>(X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+  }
+}
+
 void set_gemm_variant(int v) { g_variant = v; }
+
+void launch_gemm_nt(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* R, int ldr,
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  // measured on MI355X (tools/gemm_bench.py, K = 256): channel rows (>= 64K) take
+  // 128x128 tiles of 32x64 waves when N is a multiple of 256, else 64x64 tiles;
+  // log-psi rows take 64x128 tiles at N = 256 and 64x64 tiles otherwise.
+  int v;
+  if (g_variant >= 100) {
+    v = g_variant - 100;
+  } else if (rows >= 65536) {
+    v = (ncols % 256 == 0) ? 6 : 7;
+  } else {
+    v = (ncols == 256) ? 4 : 7;
+  }
+  launch_gemm_nt_variant(v, X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+}
+
+namespace {
+__global__ void transpose_kernel(const float* __restrict__ src, int ld_src, int rows, int cols, float* dst,
+                                 int ld_dst) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < rows && c < cols) ? src[(size_t)r * ld_src + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[(size_t)c * ld_dst + r] = t[tx][i];
+  }
+}
+}  // namespace
+
+void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s) {
+  hipLaunchKernelGGL(transpose_kernel, dim3((cols + 31) / 32, (rows + 31) / 32), dim3(256), 0, s, src, ld_src, rows,
+                     cols, dst, ld_dst);
+}
 
 void launch_gemm(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R, int ldr,
                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {

@@ -174,7 +174,9 @@ int dh_profile_read(dh_handle* h, double* out, int reset);
 int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t ws_bytes, void* stream);
 size_t dh_debug_f_offset(const dh_handle* h, int B, int op);
 /* Test hook: one launch of GEMM kernel variant `variant` (-1 = default):
- * Y = X W (+ bias on rows r % C == 0) (+ R).  X must hold round_up(rows, 256) rows. */
+ * Y = X W (+ bias on rows r % C == 0) (+ R).  X must hold round_up(rows, 256) rows.
+ * variant >= 100 selects the NT kernels: W is then the TRANSPOSED weight Wt[n][k]
+ * (row stride ldw) holding round_up(ncols, 256) rows, and K % 32 == 0. */
 int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
                   int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream);
 

@@ -14,6 +14,7 @@ lib = _lib.load()
 SHAPES = {
     "fwd_qkv": (24576, 768, 256, 1),
     "fwd_d": (24576, 256, 256, 1),
+    "fwd_orb": (24576, 192, 256, 1),
     "el_qkv": (417792, 768, 256, 17),
     "el_d": (417792, 256, 256, 17),
     "el_orb": (417792, 192, 256, 17),
@@ -32,7 +33,12 @@ def run(variant, rows, ncols, K, Cc, reps=20, check=False, residual=False):
     R = torch.randn(rp, ncols, device="cuda") if residual else None
     Y = torch.empty(rp, ncols, device="cuda")
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    args = (variant, p(X), K, p(W), ncols, p(b), p(R), ncols, p(Y), ncols, rows, ncols, K, Cc, s)
+    if variant >= 100:  # NT kernels take the transposed weight, rows padded to 256
+        Wt = torch.zeros((ncols + 255) // 256 * 256, K, device="cuda")
+        Wt[:ncols] = W.t()
+        args = (variant, p(X), K, p(Wt), K, p(b), p(R), ncols, p(Y), ncols, rows, ncols, K, Cc, s)
+    else:
+        args = (variant, p(X), K, p(W), ncols, p(b), p(R), ncols, p(Y), ncols, rows, ncols, K, Cc, s)
     assert lib.dh_debug_gemm(*args) == 0
     if check:
         ref = X[:rows].double() @ W.double()
@@ -58,7 +64,7 @@ if __name__ == "__main__":
         line = [f"{name:8s}"]
         for v in variants:
             try:
-                ms, tf = run(v, rows, n, k, cc, check=True, residual=name == "el_d")
+                ms, tf = run(v, rows, n, k, cc, check=True, residual=name in ("el_d", "fwd_d"))
                 line.append(f"v{v}: {ms * 1e3:8.1f}us {tf:6.1f}TF")
             except AssertionError as e:
                 line.append(f"v{v}: WRONG {e}")
