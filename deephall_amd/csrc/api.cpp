@@ -308,18 +308,23 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     else
       launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
   };
+  // Layer-1 q|k|v come straight from the K=4 features through the folded W0 Wqkv: inside
+  // the attention kernel when it supports that (fused), else written by the input kernel.
+  const bool fold = d.L > 0;
+  const bool fused = fold && attention_takes_features(d);
   {
-    const bool fold = d.L > 0;  // layer-1 q|k|v straight from the features (K = 4)
-    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (fold ? 4 : 1), f4 * R * DD * (fold ? 4 : 1));
-    launch_input(d, x, P.W0, fold ? P.W0qkv : nullptr, fold ? P.layer[0].bqkv : nullptr, w.h, fold ? w.qkv : nullptr,
+    const bool wq = fold && !fused;
+    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
+    launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, w.h, wq ? w.qkv : nullptr,
                  w.geo, nw, C, s);
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
     if (l > 0) gemm(w.h, D, lp.Wqkv, lp.WqkvT, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
-      PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 4.0 * DD);
-      launch_attention(d, w.qkv, w.geo, w.o, nw, C, s);
+      const bool f = fused && l == 0;
+      PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
+      launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
     gemm(w.o, D, lp.Wol, lp.WolT, D, lp.bol, w.h, D, w.t, D, D, D);

@@ -597,10 +597,53 @@ __global__ __launch_bounds__(256) void attention_ch_kernel(const float* __restri
 // registers), lane = (score pair, quarter of d) for the scores (16-byte LDS reads).
 // LDS is private to the wave; LDS ops of one wave execute in order, so a
 // __builtin_amdgcn_wave_barrier() (compiler ordering) separates the phases.
-template <int N>
+//
+// FEAT (layer 1 only): q|k|v are not read from memory but formed in registers from the
+// input-feature channels of every electron (see input.hip for the channel seeds) times
+// the folded W0 Wqkv (+ bias on the value channel) — the K=4 input map fused into the
+// attention, so the 3D-wide q|k|v rows of all channels never touch HBM.
+
+// Input-feature channel c of electron i from its geometry g = (st, ct, sp, cp):
+// [z, x, y, spin] order of psiformer.py:51-60, derivative seeds as in input.hip.
+template <int T>
+__device__ __forceinline__ float4 feature_channel(int c, int i, float4 g, float spin) {
+  const float st = g.x, ct = g.y, sp = g.z, cp = g.w;
+  if (c == 0) return make_float4(ct, st * cp, st * sp, spin);
+  if (c <= T) {
+    const int t = c - 1;
+    if ((t >> 1) != i) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
+  }
+  const float rz = ct, rx = st * cp, ry = st * sp;
+  if (c == T + 1) return make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
+  const int k = c - T - 2;  // rotation flow about axis k (0:x 1:y 2:z)
+  return make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
+}
+
+// Per-lane slice of the folded layer-1 projection: column (h, lane) of q, k and v.
+struct FeatW {
+  float4 wq, wk, wv;
+  float bq, bk, bv;
+  __device__ void load(const float* W0qkv, const float* bqkv, int D, int col) {
+    const int ld = 3 * D;
+    wq = make_float4(W0qkv[col], W0qkv[ld + col], W0qkv[2 * ld + col], W0qkv[3 * ld + col]);
+    wk = make_float4(W0qkv[D + col], W0qkv[ld + D + col], W0qkv[2 * ld + D + col], W0qkv[3 * ld + D + col]);
+    wv = make_float4(W0qkv[2 * D + col], W0qkv[ld + 2 * D + col], W0qkv[2 * ld + 2 * D + col],
+                     W0qkv[3 * ld + 2 * D + col]);
+    bq = bqkv[col];
+    bk = bqkv[D + col];
+    bv = bqkv[2 * D + col];
+  }
+  __device__ __forceinline__ static float dot(float4 f, float4 w) {
+    return fmaf(f.x, w.x, fmaf(f.y, w.y, fmaf(f.z, w.z, f.w * w.w)));
+  }
+};
+
+template <int N, bool FEAT>
 __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restrict__ qkv,
                                                             const float* __restrict__ geo, float* __restrict__ o,
-                                                            int H) {
+                                                            int H, const float* __restrict__ W0qkv,
+                                                            const float* __restrict__ bqkv, int n_up) {
   constexpr int dh = 64, ld = 68, T = 2 * N, C = 2 * N + 5, nn = N * N;
   extern __shared__ float sm[];
   float *q0 = sm, *k0 = q0 + N * ld, *v0 = k0 + N * ld, *qc = v0 + N * ld, *kc = qc + N * ld, *vc = kc + N * ld;
@@ -611,13 +654,28 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
   const float scale = 0.125f;  // 1 / sqrt(64)
   const float* base = qkv + (size_t)b * N * C * (3 * D) + h * dh + lane;
   float pq[N], pk[N], pv[N];
+  FeatW fw;
+  float4 gi[N];
+  if constexpr (FEAT) {
+    fw.load(W0qkv, bqkv, D, h * dh + lane);
+#pragma unroll
+    for (int i = 0; i < N; ++i) gi[i] = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+  }
   auto prefetch = [&](int c) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const float* r = base + (size_t)(i * C + c) * (3 * D);
-      pq[i] = r[0];
-      pk[i] = r[D];
-      pv[i] = r[2 * D];
+      if constexpr (FEAT) {
+        const float4 f = feature_channel<T>(c, i, gi[i], (i < n_up) ? 1.f : -1.f);
+        const bool v = c == 0;
+        pq[i] = FeatW::dot(f, fw.wq) + (v ? fw.bq : 0.f);
+        pk[i] = FeatW::dot(f, fw.wk) + (v ? fw.bk : 0.f);
+        pv[i] = FeatW::dot(f, fw.wv) + (v ? fw.bv : 0.f);
+      } else {
+        const float* r = base + (size_t)(i * C + c) * (3 * D);
+        pq[i] = r[0];
+        pk[i] = r[D];
+        pv[i] = r[2 * D];
+      }
     }
   };
   auto commit = [&](float* qd, float* kd, float* vd) {
@@ -825,11 +883,115 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Value-only kernel (log psi, N <= 8, dh = 64): one wave per (walker, head), four waves
+// per workgroup, no block barriers.  Lane = feature column; q|k staged in the wave's LDS
+// for the N x N scores (4 lanes per pair, 16-byte reads); v stays in registers.
+template <int N, bool FEAT>
+__global__ __launch_bounds__(256) void attention_val_kernel(const float* __restrict__ qkv,
+                                                            const float* __restrict__ geo, float* __restrict__ o,
+                                                            int H, int ntask, const float* __restrict__ W0qkv,
+                                                            const float* __restrict__ bqkv, int n_up) {
+  constexpr int dh = 64, ld = 68, nn = N * N, PER = 2 * N * ld + nn;
+  extern __shared__ float sm[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int task = blockIdx.x * 4 + w;
+  if (task >= ntask) return;  // the whole wave leaves; nothing below synchronises waves
+  float* qs = sm + w * PER;
+  float* ks = qs + N * ld;
+  float* A = ks + N * ld;
+  const int b = task / H, h = task - (task / H) * H;
+  const int D = H * dh;
+  float pq[N], pk[N], pv[N];
+  if constexpr (FEAT) {
+    FeatW fw;
+    fw.load(W0qkv, bqkv, D, h * dh + lane);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+      const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (i < n_up) ? 1.f : -1.f);
+      pq[i] = FeatW::dot(f, fw.wq) + fw.bq;
+      pk[i] = FeatW::dot(f, fw.wk) + fw.bk;
+      pv[i] = FeatW::dot(f, fw.wv) + fw.bv;
+    }
+  } else {
+    const float* base = qkv + (size_t)b * N * (3 * D) + h * dh + lane;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      pq[i] = base[(size_t)i * 3 * D];
+      pk[i] = base[(size_t)i * 3 * D + D];
+      pv[i] = base[(size_t)i * 3 * D + 2 * D];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    qs[i * ld + lane] = pq[i];
+    ks[i * ld + lane] = pk[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int p = lane; p < 4 * nn; p += 64) {
+    const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
+    const float* x = qs + i * ld + 16 * qt;
+    const float* y = ks + j * ld + 16 * qt;
+    float sdot = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 a = *reinterpret_cast<const float4*>(x + 4 * m);
+      const float4 c = *reinterpret_cast<const float4*>(y + 4 * m);
+      sdot = fmaf(a.x, c.x, fmaf(a.y, c.y, fmaf(a.z, c.z, fmaf(a.w, c.w, sdot))));
+    }
+    sdot += __shfl_xor(sdot, 1, 64);
+    sdot += __shfl_xor(sdot, 2, 64);
+    if (qt == 0) A[pair] = sdot * 0.125f;  // 1 / sqrt(64)
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < N) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A[lane * N + j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A[lane * N + j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A[lane * N + j] = e[j] * inv;
+  }
+  __builtin_amdgcn_wave_barrier();
+  float* ob = o + (size_t)b * N * D + h * dh + lane;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc = fmaf(A[i * N + j], pv[j], acc);
+    ob[(size_t)i * D] = acc;
+  }
+}
+
 template <int N>
-void launch_wave(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s) {
+void launch_wave(const Dims& d, const float* qkv, const float* W0qkv, const float* bqkv, const float* geo, float* o,
+                 int nw, int C, hipStream_t s) {
   const int nn = N * N;
+  if (C == 1) {
+    const int ntask = nw * d.H;
+    const size_t smem = (size_t)4 * (2 * N * 68 + nn) * sizeof(float);
+    if (W0qkv)
+      hipLaunchKernelGGL((attention_val_kernel<N, true>), dim3((ntask + 3) / 4), dim3(256), smem, s, qkv, geo, o,
+                         d.H, ntask, W0qkv, bqkv, d.n_up);
+    else
+      hipLaunchKernelGGL((attention_val_kernel<N, false>), dim3((ntask + 3) / 4), dim3(256), smem, s, qkv, geo, o,
+                         d.H, ntask, W0qkv, bqkv, d.n_up);
+    return;
+  }
   const size_t smem = (size_t)(6 * N * 68 + 15 * nn + 6 * N) * sizeof(float);
-  hipLaunchKernelGGL(attention_wave_kernel<N>, dim3(nw * d.H), dim3(64), smem, s, qkv, geo, o, d.H);
+  if (W0qkv)
+    hipLaunchKernelGGL((attention_wave_kernel<N, true>), dim3(nw * d.H), dim3(64), smem, s, qkv, geo, o, d.H, W0qkv,
+                       bqkv, d.n_up);
+  else
+    hipLaunchKernelGGL((attention_wave_kernel<N, false>), dim3(nw * d.H), dim3(64), smem, s, qkv, geo, o, d.H, W0qkv,
+                       bqkv, d.n_up);
 }
 
 template <int PF, int RPT>
@@ -842,21 +1004,26 @@ void launch_ch(const Dims& d, const float* qkv, const float* geo, float* o, int 
 
 }  // namespace
 
-void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s) {
-  // channel kernel v2 needs dh <= 64 (one feature column per lane) and dh % 4 == 0;
-  // PF = float4 prefetch slots >= 3 N dh / 1024, RPT = rows per thread >= N / 4
-  if (C > 1 && d.dh == 64 && d.N <= 8) {
+bool attention_takes_features(const Dims& d) { return d.dh == 64 && d.N <= 8; }
+
+void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
+                      const float* W0qkv, const float* bqkv) {
+  // wave kernels (value and channel) for dh = 64, N <= 8; W0qkv != nullptr selects the
+  // fused layer-1 form (q|k|v from the input features), valid only for those kernels.
+  if (attention_takes_features(d)) {
     switch (d.N) {
-      case 1: launch_wave<1>(d, qkv, geo, o, nw, s); return;
-      case 2: launch_wave<2>(d, qkv, geo, o, nw, s); return;
-      case 3: launch_wave<3>(d, qkv, geo, o, nw, s); return;
-      case 4: launch_wave<4>(d, qkv, geo, o, nw, s); return;
-      case 5: launch_wave<5>(d, qkv, geo, o, nw, s); return;
-      case 6: launch_wave<6>(d, qkv, geo, o, nw, s); return;
-      case 7: launch_wave<7>(d, qkv, geo, o, nw, s); return;
-      default: launch_wave<8>(d, qkv, geo, o, nw, s); return;
+      case 1: launch_wave<1>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 2: launch_wave<2>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 3: launch_wave<3>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 4: launch_wave<4>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 5: launch_wave<5>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 6: launch_wave<6>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 7: launch_wave<7>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      default: launch_wave<8>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
     }
   }
+  // channel kernel v2 needs dh <= 64 (one feature column per lane) and dh % 4 == 0;
+  // PF = float4 prefetch slots >= 3 N dh / 1024, RPT = rows per thread >= N / 4
   if (C > 1 && d.dh % 4 == 0 && d.dh <= 64 && d.N <= 32) {
     const int N = d.N;
     if (N <= 4)

@@ -85,7 +85,11 @@ void launch_propose(const Dims& d, const float* x, float* x2, int nw, float widt
 void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t walker_offset, hipStream_t s);
 
 // attention.hip: channel self-attention for all heads.
-void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s);
+// W0qkv/bqkv non-null: layer-1 q|k|v formed in-kernel from the input features (only when
+// attention_takes_features(d)); otherwise read from qkv [rows][3D].
+bool attention_takes_features(const Dims& d);
+void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
+                      const float* W0qkv = nullptr, const float* bqkv = nullptr);
 
 // layernorm.hip
 //   mode 0: h = LN_ch(X)           (X may alias h)
