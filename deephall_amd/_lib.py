@@ -44,6 +44,7 @@ EXPORTS = [
     "dh_potential",
     "dh_debug_trunk",
     "dh_debug_gemm",
+    "dh_debug_gemm_ln",
     "dh_profile_enable",
     "dh_profile_read",
     "dh_debug_f_offset",
@@ -116,6 +117,8 @@ def load(path: Path | str | None = None):
     lib.dh_debug_f_offset.restype = sz
     lib.dh_debug_gemm.argtypes = [i32, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp]
     lib.dh_debug_gemm.restype = i32
+    lib.dh_debug_gemm_ln.argtypes = [i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp]
+    lib.dh_debug_gemm_ln.restype = i32
     lib.dh_profile_enable.argtypes = [vp, i32]
     lib.dh_profile_enable.restype = i32
     lib.dh_profile_read.argtypes = [vp, C.POINTER(C.c_double), i32]

@@ -300,6 +300,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const int D = d.D;
   const double R = rows, DD = D, f4 = 4.0;
   const bool nt = P.WorbT != nullptr;
+  const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
   auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, int ldw, const float* bias,
                   const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
     PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
@@ -325,6 +326,18 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
+    }
+    if (ln_fused) {
+      // log psi: each GEMM carries its LayerNorm in the epilogue, in place over h
+      {
+        PROF(PK_GEMM, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
+        launch_gemm_ln(w.o, D, lp.WolT, D, lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
+      }
+      {
+        PROF(PK_GEMM, 2.0 * R * DD * DD, f4 * (2.0 * R * DD + DD * DD));
+        launch_gemm_ln(w.h, D, lp.WmT, D, lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
+      }
+      continue;
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
     gemm(w.o, D, lp.Wol, lp.WolT, D, lp.bol, w.h, D, w.t, D, D, D);
@@ -466,6 +479,13 @@ int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw,
     launch_gemm_variant(variant < 0 ? 0 : variant, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
                         (hipStream_t)stream);
   }
+  return check_launch();
+}
+
+int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
+                     const float* ln, float* h, int rows, int K, void* stream) {
+  if (!gemm_ln_supported(256, K) || rows < 1 || (mode != 0 && mode != 1)) return fail(DH_EINVAL, "bad gemm_ln args");
+  launch_gemm_ln(X, ldx, Wt, ldw, bias, ln, h, rows, K, mode, bm, (hipStream_t)stream);
   return check_launch();
 }
 

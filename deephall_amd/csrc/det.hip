@@ -256,13 +256,28 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
 
 // ------------------------------------------------------------------ energy kernel
 struct DetSmem {
-  int geo, alpha, E0, DTH, DPH, LB, D2TH, Aug, Binv, Phi, Mt, Mu, Gu, fac, ellt, ell0, ellL, ellS, red, misc, total;
+  int geo, alpha, E0, DTH, DPH, LB, D2TH, Aug, Binv, Phi, Mt, Mu, Gu, fac, ellt, ell0, ellL, ellS, red, misc;
+  int Fv, Fc, LB2, asmb, total;  // staged orbital rows (value, current channel); own-tangent LB terms;
+                                 // double-precision assembly partials
 };
+// Orbital rows are staged through LDS when the N rows of one channel (the electron's own
+// spin block: 2 M N K floats each) fit this many floats.
+constexpr int kStageFloats = 5120;
+__host__ __device__ inline bool det_staged(int N, int M, int K) { return 2 * M * N * K * N <= kStageFloats; }
 __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
   // offsets in floats; complex arrays take 2 floats per element
   DetSmem L;
   const int T = 2 * N, NN = N * N;
   int o = 0;
+  const int rows = det_staged(N, M, K) ? 2 * M * N * K * N : 0;
+  L.Fv = o;
+  o += rows;
+  L.Fc = o;
+  o += rows;
+  L.LB2 = o;
+  o += 2 * NN;
+  L.asmb = o;  // even offset: doubles
+  o += 2 * (4 * T + 3 * N);
   L.geo = o;
   o += 4 * N;
   L.alpha = o;
@@ -326,7 +341,8 @@ __device__ inline void block_sum4(float v[4], float* red) {
   __syncthreads();
 }
 
-__global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+template <int PF>  // PF > 0: orbital rows staged through LDS, PF floats per thread in flight
+__global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                   const float* __restrict__ geo_g, const float* __restrict__ jas,
                                   const float* __restrict__ norm, float* __restrict__ e_l, float* __restrict__ obs,
                                   int N, int n_up, int M, int K, float Q, float radius, float lambda,
@@ -347,6 +363,44 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
   int* piv = reinterpret_cast<int*>(sm + L.misc);
   cf* logdet = reinterpret_cast<cf*>(sm + L.misc + 2);
   const FView F{Fp, ldF, M, N, K};
+  const size_t rowbase = (size_t)b * N * C;  // row of (b, i, c) = rowbase + i*C + c
+  // ---- staging of orbital rows (STAGED): the N rows of one channel, each the electron's
+  // own spin block (2 M N K floats), through registers into LDS.  The value rows stay in
+  // Fv; channel c's rows go to Fc while channel c+1's are already in flight.
+  const int MNK = M * N * K, RW = 2 * MNK, NRW = N * RW;
+  float* Fv = sm + L.Fv;
+  float* Fc = sm + L.Fc;
+  cf* LB2 = (cf*)(sm + L.LB2);
+  constexpr bool STAGED = PF > 0;
+  constexpr int PFMAX = STAGED ? PF : 1;
+  float pf[PFMAX];
+  auto stage_load = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < PFMAX; ++u) {
+      const int q = tid + u * nt;
+      if (q < NRW) {
+        const int i = q / RW, w = q - (q / RW) * RW;
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        pf[u] = Fp[(rowbase + (size_t)i * C + c) * ldF + (size_t)blk * RW + w];
+      }
+    }
+  };
+  auto stage_store = [&](float* dst) {
+#pragma unroll
+    for (int u = 0; u < PFMAX; ++u) {
+      const int q = tid + u * nt;
+      if (q < NRW) dst[q] = pf[u];
+    }
+  };
+  // element (part re/im of) orbital m, column j, det kd of electron i from a staged buffer
+  auto fs = [&](const float* buf, int i, int p, int j, int kd) -> cf {
+    const float* r = buf + i * RW + (p * N + j) * K + kd;
+    return cf{r[0], r[MNK]};
+  };
+  if constexpr (STAGED) {
+    stage_load(0);
+    stage_store(Fv);
+  }
 
   for (int i = tid; i < N; i += nt) {
     const float4 g = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
@@ -380,14 +434,18 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
   }
   __syncthreads();
 
-  const size_t rowbase = (size_t)b * N * C;  // row of (b, i, c) = rowbase + i*C + c
   for (int kd = 0; kd < K; ++kd) {
+    if constexpr (STAGED) {
+      stage_load(1);  // first tangent channel, in flight during the LU below
+      for (int idx = tid; idx < NN; idx += nt) LB2[idx] = cf{0.f, 0.f};
+    }
     // ---- Phi0 and its inverse (augmented Gauss-Jordan)
     for (int idx = tid; idx < NN; idx += nt) {
       const int i = idx / N, j = idx % N;
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       cf acc{0.f, 0.f};
-      for (int p = 0; p < M; ++p) cfma(acc, F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
+      for (int p = 0; p < M; ++p)
+        cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
       Aug[i * 2 * N + j] = acc;
       Aug[i * 2 * N + N + j] = (i == j) ? cf{1.f, 0.f} : cf{0.f, 0.f};
     }
@@ -407,6 +465,11 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
       const int it = t >> 1;
       const cf* dE = (t & 1) ? DPH : DTH;
       const float a0 = al[t], a1 = al[T + t], a2 = al[2 * T + t];
+      if constexpr (STAGED) {  // Fc <- channel 1+t (readers of the previous channel are done)
+        stage_store(Fc);
+        stage_load(t + 1 < T ? t + 2 : T + 1);
+        __syncthreads();
+      }
       for (int idx = tid; idx < NN; idx += nt) {
         const int i = idx / N, j = idx % N;
         const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
@@ -415,9 +478,11 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
         const float phh[3] = {-sp, cp, 0.f};
         const float thh[3] = {ct * cp, ct * sp, -st};
         cf acc{0.f, 0.f}, g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
+        cf lb2{0.f, 0.f};
         for (int p = 0; p < M; ++p) {
-          const cf f = F.at(rt, blk, p, j, kd);
+          const cf f = STAGED ? fs(Fc, i, p, j, kd) : F.at(rt, blk, p, j, kd);
           const cf dth = DTH[i * M + p], dph = DPH[i * M + p];
+          if (STAGED && i == it) cfma(lb2, f, (t & 1) ? dph : dth);
           cfma(acc, f, E0[i * M + p]);
           cfma(g0, f, phh[0] * dth - thh[0] * dph);
           cfma(g1, f, phh[1] * dth - thh[1] * dph);
@@ -425,7 +490,9 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
         }
         if (i == it) {
           const size_t r0 = rowbase + (size_t)i * C;
-          for (int p = 0; p < M; ++p) cfma(acc, F.at(r0, blk, p, j, kd), dE[i * M + p]);
+          for (int p = 0; p < M; ++p)
+            cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(r0, blk, p, j, kd), dE[i * M + p]);
+          if (STAGED) LB2[idx] += lb2;  // own-tangent term of the Laplace-Beltrami channel
         }
         Phi[idx] = acc;
         Gu[idx] += a0 * g0;
@@ -462,17 +529,30 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
 
     // ---- Laplace-Beltrami channel
     {
+      if constexpr (STAGED) {
+        stage_store(Fc);
+        stage_load(T + 2);
+        __syncthreads();
+      }
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       for (int idx = tid; idx < NN; idx += nt) {
         const int i = idx / N, j = idx % N;
         const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
         const size_t r0 = rowbase + (size_t)i * C;
         cf acc{0.f, 0.f}, acc2{0.f, 0.f};
-        for (int p = 0; p < M; ++p) {
-          cfma(acc, F.at(r0 + 1 + T, blk, p, j, kd), E0[i * M + p]);
-          cfma(acc, F.at(r0, blk, p, j, kd), LBe[i * M + p]);
-          cfma(acc2, F.at(r0 + 1 + 2 * i, blk, p, j, kd), DTH[i * M + p]);
-          cfma(acc2, F.at(r0 + 2 + 2 * i, blk, p, j, kd), DPH[i * M + p]);
+        if constexpr (STAGED) {
+          for (int p = 0; p < M; ++p) {
+            cfma(acc, fs(Fc, i, p, j, kd), E0[i * M + p]);
+            cfma(acc, fs(Fv, i, p, j, kd), LBe[i * M + p]);
+          }
+          acc2 = LB2[idx];
+        } else {
+          for (int p = 0; p < M; ++p) {
+            cfma(acc, F.at(r0 + 1 + T, blk, p, j, kd), E0[i * M + p]);
+            cfma(acc, F.at(r0, blk, p, j, kd), LBe[i * M + p]);
+            cfma(acc2, F.at(r0 + 1 + 2 * i, blk, p, j, kd), DTH[i * M + p]);
+            cfma(acc2, F.at(r0 + 2 + 2 * i, blk, p, j, kd), DPH[i * M + p]);
+          }
         }
         acc += 2.f * acc2;
         // tr(B Phi) = sum_ij B[j][i] Phi[i][j]
@@ -485,6 +565,11 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
     }
     // ---- flow channels
     for (int k = 0; k < 3; ++k) {
+      if constexpr (STAGED) {
+        stage_store(Fc);
+        if (k < 2) stage_load(T + 3 + k);
+        __syncthreads();
+      }
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       for (int idx = tid; idx < NN; idx += nt) {
         const int i = idx / N, j = idx % N;
@@ -495,8 +580,8 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
         for (int p = 0; p < M; ++p) {
           const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
           const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
-          cfma(acc, F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
-          cfma(acc, F.at(r0, blk, p, j, kd), sf);
+          cfma(acc, STAGED ? fs(Fc, i, p, j, kd) : F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
+          cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(r0, blk, p, j, kd), sf);
         }
         acc += 2.f * Gu[k * NN + idx];
         const cf pr = Binv[j * N + i] * acc;
@@ -512,133 +597,165 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
     __syncthreads();
   }
 
-  // ---- combine determinants, Jastrow, potential, assembly (thread 0, double precision)
-  if (tid == 0) {
-    double lmax = -1e300;
-    for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
-    double wr[16], wi[16];
-    double zr = 0.0, zi = 0.0;
+  // ---- combine determinants, Jastrow, potential, assembly (double precision).
+  // Per-tangent terms on threads t < T, per-electron Jastrow / potential sums on threads
+  // T + i, partial results in LDS; thread 0 finishes with scalar sums only (no private
+  // arrays, so nothing goes to scratch memory).
+  __syncthreads();  // ell* written by thread 0 in the channel loops
+  double* tgr = reinterpret_cast<double*>(sm + L.asmb);
+  double* tgi = tgr + T;
+  double* lbr = tgi + T;
+  double* lbi = lbr + T;
+  double* Jn = lbi + T;
+  double* Jlbn = Jn + N;
+  double* pen = Jlbn + N;
+  // determinant weights p_k = w_k / Z, w_k = exp(ell0_k - max) (every thread; K is small)
+  double lmax = -1e300;
+  for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
+  double zr = 0.0, zi = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double mag = exp((double)ell0[k].re - lmax);
+    zr += mag * cos((double)ell0[k].im);
+    zi += mag * sin((double)ell0[k].im);
+  }
+  const double zz = zr * zr + zi * zi;
+  auto pk = [&](int k, double& pr, double& pi_) {
+    const double mag = exp((double)ell0[k].re - lmax);
+    const double wr = mag * cos((double)ell0[k].im), wi = mag * sin((double)ell0[k].im);
+    pr = (wr * zr + wi * zi) / zz;
+    pi_ = (wi * zr - wr * zi) / zz;
+  };
+  const double ap = jas[0], aa = jas[1];
+  if (tid < T) {
+    const int t = tid, i = t >> 1;
+    double gr = 0.0, gi = 0.0, sr = 0.0, si = 0.0;
     for (int k = 0; k < K; ++k) {
-      const double mag = exp((double)ell0[k].re - lmax);
-      wr[k] = mag * cos((double)ell0[k].im);
-      wi[k] = mag * sin((double)ell0[k].im);
-      zr += wr[k];
-      zi += wi[k];
+      double pr, pi_;
+      pk(k, pr, pi_);
+      const double lr = ellt[k * T + t].re, li = ellt[k * T + t].im;
+      gr += pr * lr - pi_ * li;
+      gi += pr * li + pi_ * lr;
+      const double l2r = lr * lr - li * li, l2i = 2.0 * lr * li;
+      sr += pr * l2r - pi_ * l2i;
+      si += pr * l2i + pi_ * l2r;
     }
-    const double zz = zr * zr + zi * zi;
-    for (int k = 0; k < K; ++k) {  // p_k = w_k / Z
-      const double pr = (wr[k] * zr + wi[k] * zi) / zz, pi_ = (wi[k] * zr - wr[k] * zi) / zz;
-      wr[k] = pr;
-      wi[k] = pi_;
+    lbr[t] = sr - (gr * gr - gi * gi);
+    lbi[t] = si - 2.0 * gr * gi;
+    // Jastrow gradient along the (scaled) tangent t of electron i
+    const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
+    const double ri[3] = {sti * cpi, sti * spi, cti};
+    const double et[3] = {(t & 1) ? -spi : cti * cpi, (t & 1) ? cpi : cti * spi, (t & 1) ? 0.0 : -sti};
+    double jg = 0.0;
+    for (int j = 0; j < N; ++j) {
+      if (j == i) continue;
+      const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
+      const double rj[3] = {stj * cpj, stj * spj, ctj};
+      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
+      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
+      const bool same = (i < n_up) == (j < n_up);
+      double f1, f2;
+      (void)jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+      jg += (-f1 / r) * (rj[0] * et[0] + rj[1] * et[1] + rj[2] * et[2]);
     }
+    // gauge term A = i Q sum_i sigma_i phi_i (env_leaf) on the phi tangent
+    if (t & 1) gi += Q * ((cti >= 0.0) ? 1.0 : -1.0) / sti;
+    tgr[t] = gr + jg;
+    tgi[t] = gi;
+  } else if (tid < T + N) {
+    const int i = tid - T;
+    const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
+    const double ri[3] = {sti * cpi, sti * spi, cti};
+    double J = 0.0, Jlb = 0.0, pe = 0.0;
+    for (int j = i + 1; j < N; ++j) {
+      const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
+      const double rj[3] = {stj * cpj, stj * spj, ctj};
+      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
+      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
+      const bool same = (i < n_up) == (j < n_up);
+      double f1, f2;
+      J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+      Jlb += 2.0 * ((4.0 - r * r) * r * f2 + (4.0 - 3.0 * r * r) * f1) / (4.0 * r);
+      if (interaction == DH_INTERACTION_COULOMB)
+        pe += 1.0 / sqrt(2.0 - 2.0 * u);
+      else
+        pe += 1.0 + ((double)Q + 1.0) / (double)Q * u;
+    }
+    Jn[i] = J;
+    Jlbn[i] = Jlb;
+    pen[i] = pe;
+  }
+  __syncthreads();
+  if (tid == 0) {
     const double val_re = 0.5 * log(zz) + lmax, val_im = atan2(zi, zr);
-    // g1_t and Laplacian combination
-    double tg_re[64], tg_im[64];
     double LB_re = 0.0, LB_im = 0.0;
     for (int k = 0; k < K; ++k) {
-      LB_re += wr[k] * ellL[k].re - wi[k] * ellL[k].im;
-      LB_im += wr[k] * ellL[k].im + wi[k] * ellL[k].re;
+      double pr, pi_;
+      pk(k, pr, pi_);
+      LB_re += pr * ellL[k].re - pi_ * ellL[k].im;
+      LB_im += pr * ellL[k].im + pi_ * ellL[k].re;
     }
     for (int t = 0; t < T; ++t) {
-      double gr = 0.0, gi = 0.0, sr = 0.0, si = 0.0;
-      for (int k = 0; k < K; ++k) {
-        const double lr = ellt[k * T + t].re, li = ellt[k * T + t].im;
-        gr += wr[k] * lr - wi[k] * li;
-        gi += wr[k] * li + wi[k] * lr;
-        const double l2r = lr * lr - li * li, l2i = 2.0 * lr * li;
-        sr += wr[k] * l2r - wi[k] * l2i;
-        si += wr[k] * l2i + wi[k] * l2r;
-      }
-      tg_re[t] = gr;
-      tg_im[t] = gi;
-      LB_re += sr - (gr * gr - gi * gi);
-      LB_im += si - 2.0 * gr * gi;
+      LB_re += lbr[t];
+      LB_im += lbi[t];
     }
     double S_re[3], S_im[3];
+#pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
       double a_r = 0.0, a_i = 0.0, m1r = 0.0, m1i = 0.0, m2r = 0.0, m2i = 0.0;
       for (int k = 0; k < K; ++k) {
-        a_r += wr[k] * ellS[3 * k + kk].re - wi[k] * ellS[3 * k + kk].im;
-        a_i += wr[k] * ellS[3 * k + kk].im + wi[k] * ellS[3 * k + kk].re;
+        double pr, pi_;
+        pk(k, pr, pi_);
+        a_r += pr * ellS[3 * k + kk].re - pi_ * ellS[3 * k + kk].im;
+        a_i += pr * ellS[3 * k + kk].im + pi_ * ellS[3 * k + kk].re;
         double gur = 0.0, gui = 0.0;
         for (int t = 0; t < T; ++t) {
           gur += (double)al[kk * T + t] * ellt[k * T + t].re;
           gui += (double)al[kk * T + t] * ellt[k * T + t].im;
         }
-        m1r += wr[k] * gur - wi[k] * gui;
-        m1i += wr[k] * gui + wi[k] * gur;
+        m1r += pr * gur - pi_ * gui;
+        m1i += pr * gui + pi_ * gur;
         const double g2r = gur * gur - gui * gui, g2i = 2.0 * gur * gui;
-        m2r += wr[k] * g2r - wi[k] * g2i;
-        m2i += wr[k] * g2i + wi[k] * g2r;
+        m2r += pr * g2r - pi_ * g2i;
+        m2i += pr * g2i + pi_ * g2r;
       }
       S_re[kk] = a_r + m2r - (m1r * m1r - m1i * m1i);
       S_im[kk] = a_i + m2i - 2.0 * m1r * m1i;
     }
-    // Jastrow value, gradient (scaled basis) and Laplace-Beltrami; potential
     double J = 0.0, Jlb = 0.0, pe = 0.0;
-    double Jg[64];
-    for (int t = 0; t < T; ++t) Jg[t] = 0.0;
-    const double ap = jas[0], aa = jas[1];
     for (int i = 0; i < N; ++i) {
-      const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
-      const double ri[3] = {sti * cpi, sti * spi, cti};
-      const double thi[3] = {cti * cpi, cti * spi, -sti};
-      const double phi_[3] = {-spi, cpi, 0.0};
-      for (int j = i + 1; j < N; ++j) {
-        const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
-        const double rj[3] = {stj * cpj, stj * spj, ctj};
-        const double thj[3] = {ctj * cpj, ctj * spj, -stj};
-        const double phj[3] = {-spj, cpj, 0.0};
-        const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
-        const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
-        const bool same = (i < n_up) == (j < n_up);
-        double f1, f2;
-        J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
-        const double gu = -f1 / r;
-        Jg[2 * i] += gu * (rj[0] * thi[0] + rj[1] * thi[1] + rj[2] * thi[2]);
-        Jg[2 * i + 1] += gu * (rj[0] * phi_[0] + rj[1] * phi_[1] + rj[2] * phi_[2]);
-        Jg[2 * j] += gu * (ri[0] * thj[0] + ri[1] * thj[1] + ri[2] * thj[2]);
-        Jg[2 * j + 1] += gu * (ri[0] * phj[0] + ri[1] * phj[1] + ri[2] * phj[2]);
-        Jlb += 2.0 * ((4.0 - r * r) * r * f2 + (4.0 - 3.0 * r * r) * f1) / (4.0 * r);
-        if (interaction == DH_INTERACTION_COULOMB)
-          pe += 1.0 / sqrt(2.0 - 2.0 * u);
-        else
-          pe += 1.0 + ((double)Q + 1.0) / (double)Q * u;
-      }
+      J += Jn[i];
+      Jlb += Jlbn[i];
+      pe += pen[i];
     }
     if (interaction == DH_INTERACTION_COULOMB) pe /= (double)radius;
-    // gauge term A = i Q sum_i sigma_i phi_i (env_leaf): tangents, flow channels, phase
+    // gauge terms: phase and the flow channels' phi acceleration (see env_flow2)
     double gauge_phase = 0.0;
     for (int i = 0; i < N; ++i) {
       const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
-      const double sg = (geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0;
-      tg_im[2 * i + 1] += Q * sg / st;
+      const double sg = (ct >= 0.0) ? 1.0 : -1.0;
       gauge_phase += Q * sg * (double)x[2 * (b * N + i) + 1];
       const double cot = ct / st;
-      // phi acceleration along the three rotation flows (see env_flow2)
       const double tdot[3] = {-sp, cp, 0.0};
       const double thp[3] = {cp * cot, sp * cot, -1.0};
       const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
       const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
+#pragma unroll
       for (int kk = 0; kk < 3; ++kk) S_im[kk] += Q * sg * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
     }
     pe *= (double)lambda;
     LB_re += Jlb;
-    // assembly
     double sq_re = 0.0, sq_im = 0.0, mag_re = 0.0, mag_im = 0.0;
     for (int t = 0; t < T; ++t) {
-      tg_re[t] += Jg[t];
-      sq_re += tg_re[t] * tg_re[t] - tg_im[t] * tg_im[t];
-      sq_im += 2.0 * tg_re[t] * tg_im[t];
+      sq_re += tgr[t] * tgr[t] - tgi[t] * tgi[t];
+      sq_im += 2.0 * tgr[t] * tgi[t];
     }
     double Mv[3] = {0.0, 0.0, 0.0};
     for (int i = 0; i < N; ++i) {
       const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
       const double cot = ct / st;
       mag_re += (Q * cot) * (Q * cot);
-      // 2 i Q cot * t_phi_scaled
-      mag_re += -2.0 * Q * cot * tg_im[2 * i + 1];
-      mag_im += 2.0 * Q * cot * tg_re[2 * i + 1];
+      mag_re += -2.0 * Q * cot * tgi[2 * i + 1];  // 2 i Q cot * t_phi_scaled
+      mag_im += 2.0 * Q * cot * tgr[2 * i + 1];
       Mv[0] += Q * cp / st;
       Mv[1] += Q * sp / st;
     }
@@ -646,19 +763,20 @@ __global__ void det_energy_kernel(const float* __restrict__ Fp, int ldF, const f
     const double ke_re = (-LB_re - sq_re + mag_re) / (2.0 * r2);
     const double ke_im = (-LB_im - sq_im + mag_im) / (2.0 * r2);
     double G_re[3], G_im[3];
+#pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
       double gr = 0.0, gi = 0.0;
       for (int t = 0; t < T; ++t) {
-        gr += (double)al[kk * T + t] * tg_re[t];
-        gi += (double)al[kk * T + t] * tg_im[t];
+        gr += (double)al[kk * T + t] * tgr[t];
+        gi += (double)al[kk * T + t] * tgi[t];
       }
       G_re[kk] = gr;
       G_im[kk] = gi;
     }
     double L2 = 0.0;
+#pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
-      // (G + i M)^2, real part
-      const double ar = G_re[kk], ai = G_im[kk] + Mv[kk];
+      const double ar = G_re[kk], ai = G_im[kk] + Mv[kk];  // (G + i M)^2, real part
       L2 -= S_re[kk] + (ar * ar - ai * ai);
     }
     const double lz = G_im[2];
@@ -716,9 +834,19 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s) {
   const int threads = 256;
   const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64);
-  ensure_smem(det_energy_kernel, (size_t)L.total * sizeof(float));
-  hipLaunchKernelGGL(det_energy_kernel, dim3(nw), dim3(threads), (size_t)L.total * sizeof(float), s, F, d.ld_orb, x,
-                     geo, jastrow, norm, e_l, obs, d.N, d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction);
+  const size_t bytes = (size_t)L.total * sizeof(float);
+  const int nrw = 2 * d.M * d.N * d.K * d.N;  // floats of one channel's N staged rows
+  auto go = [&](auto kern) {
+    ensure_smem(kern, bytes);
+    hipLaunchKernelGGL(kern, dim3(nw), dim3(threads), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N,
+                       d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction);
+  };
+  if (!det_staged(d.N, d.M, d.K))
+    go(det_energy_kernel<0>);
+  else if (nrw <= 8 * threads)
+    go(det_energy_kernel<8>);
+  else
+    go(det_energy_kernel<kStageFloats / 256>);
 }
 
 size_t det_energy_smem_bytes(const Dims& d) { return (size_t)det_layout(d.N, d.M, d.K, 4).total * sizeof(float); }

@@ -1,5 +1,6 @@
 // Internal declarations shared by the HIP kernel files and the C ABI (api.cpp).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -69,6 +70,11 @@ void set_gemm_variant(int v);
 // NT GEMM with the tile shape chosen from (rows, ncols, residual): Wt[n][k], row stride ldw.
 void launch_gemm_nt(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* R, int ldr,
                     float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+// Log-psi rows (C = 1), D = 256: GEMM + bias, then (mode 0) + h or (mode 1) h + tanh(.),
+// then LayerNorm (ln = gamma|beta), written in place over h [rows][256].
+bool gemm_ln_supported(int D, int K);
+void launch_gemm_ln(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* ln, float* h,
+                    int rows, int K, int mode, int bm, hipStream_t s);
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).
 void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s);
 

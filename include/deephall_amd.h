@@ -180,6 +180,13 @@ size_t dh_debug_f_offset(const dh_handle* h, int B, int op);
 int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw, const float* bias, const float* R,
                   int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream);
 
+/* Test hook: the log-psi GEMM with the LayerNorm fused into its epilogue (D = 256):
+ * h = LN(h + X Wt^T + bias) (mode 0) or LN(h + tanh(X Wt^T + bias)) (mode 1), in place;
+ * Wt[256][K] transposed weight (row stride ldw), ln = gamma[256] | beta[256];
+ * bm = rows per workgroup (32, 64, 96; 0 = automatic).  X, h hold round_up(rows, 96) rows. */
+int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
+                     const float* ln, float* h, int rows, int K, void* stream);
+
 /* init_guess with the device RNG: theta = arccos U(-1,1), phi = U(-pi,pi). */
 int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream);
 

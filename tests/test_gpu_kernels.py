@@ -1,0 +1,103 @@
+"""GPU unit tests of the GEMM kernels through the C ABI test hooks, against float64 torch.
+
+Every tile variant of the register-staged GEMM (dh_debug_gemm 0..11), of the LDS-DMA
+NT GEMM (100+), and the log-psi GEMM with the LayerNorm fused into its epilogue
+(dh_debug_gemm_ln), on hot-path shapes including ragged rows / columns, the
+channel-row bias rule (bias on rows r % C == 0 only) and the residual.
+Tolerance: f32 products of K = 256 terms, |err| <= 2e-5 * (sum_k |x w| + 1).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import pytest
+import torch
+
+from deephall_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ref(X, W, b, R, rows, Cc):
+    y = X[:rows].double() @ W.double()
+    mask = (torch.arange(rows, device=X.device) % Cc == 0).double()[:, None]
+    if b is not None:
+        y = y + mask * b.double()
+    if R is not None:
+        y = y + R[:rows].double()
+    scale = X[:rows].double().abs() @ W.double().abs() + 1.0
+    return y, scale
+
+
+SHAPES = [(1000, 256, 256, 17), (24576 // 8, 768, 256, 1), (777, 192, 256, 17), (300, 100, 256, 1)]
+VARIANTS = list(range(12)) + [100 + v for v in (0, 1, 2, 3, 4, 5, 6, 7, 10, 11, 14, 15, 16, 17, 18)]
+PERSISTENT = [120 + v for v in range(7)]  # write padding rows / columns (Y padded to 256 x 256)
+VARIANTS += PERSISTENT
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gemm_variants(cuda, variant):
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(variant)
+    for rows, n, K, Cc in SHAPES:
+        rp = (rows + 255) // 256 * 256
+        X = torch.randn(rp, K, generator=g).cuda()
+        W = (torch.randn(K, n, generator=g) / 16).cuda()
+        b = torch.randn(n, generator=g).cuda()
+        R = torch.randn(rp, n, generator=g).cuda() if n == 256 else None
+        ldy = (n + 255) // 256 * 256 if variant in PERSISTENT else n
+        Yb = torch.full((rp, ldy), float("nan"), device="cuda")
+        Y = Yb[:, :n]
+        if variant >= 100:
+            Wt = torch.zeros((n + 255) // 256 * 256, K, device="cuda")
+            Wt[:n] = W.t()
+            rc = lib.dh_debug_gemm(variant, _p(X), K, _p(Wt), K, _p(b), _p(R), n, _p(Yb), ldy, rows, n, K, Cc,
+                                   _stream())
+        else:
+            rc = lib.dh_debug_gemm(variant, _p(X), K, _p(W), n, _p(b), _p(R), n, _p(Y), n, rows, n, K, Cc, _stream())
+        assert rc == 0
+        torch.cuda.synchronize()
+        ref, scale = _ref(X, W, b, R, rows, Cc)
+        err = ((Y[:rows].double() - ref).abs() / scale).max().item()
+        assert err < 2e-5, (variant, rows, n, err)
+        if variant not in PERSISTENT:
+            assert torch.isnan(Y[rows:]).all()  # rows past `rows` untouched
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("bm", [0, 32, 64, 96])
+@pytest.mark.parametrize("rows", [96, 1000, 24576])
+def test_gemm_layernorm_fused(cuda, mode, bm, rows):
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(17 * mode + bm + rows)
+    K, D = 256, 256
+    rp = (rows + 767) // 768 * 768  # readable rows for every tile height (lcm of 256 and 96)
+    X = torch.randn(rp, K, generator=g).cuda()
+    W = (torch.randn(K, D, generator=g) / 16).cuda()
+    Wt = W.t().contiguous()
+    b = torch.randn(D, generator=g).cuda()
+    ln = torch.cat([1.0 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)]).cuda()
+    h0 = torch.randn(rp, D, generator=g).cuda()
+    if mode == 1:
+        X = h0  # the MLP reads h and writes LN(h + tanh(h W + b)) over it
+    h = h0.clone()
+    Xin = h if mode == 1 else X
+    assert lib.dh_debug_gemm_ln(mode, bm, _p(Xin), K, _p(Wt), K, _p(b), _p(ln), _p(h), rows, K, _stream()) == 0
+    torch.cuda.synchronize()
+    z = X[:rows].double() @ W.double() + b.double()
+    y = h0[:rows].double() + (z if mode == 0 else torch.tanh(z))
+    mu = y.mean(-1, keepdim=True)
+    var = ((y - mu) ** 2).mean(-1, keepdim=True)
+    ref = (y - mu) / torch.sqrt(var + 1e-5) * ln[:D].double() + ln[D:].double()
+    err = (h[:rows].double() - ref).abs().max().item()
+    assert err < 2e-4, err
+    assert torch.equal(h[rows:], h0[rows:])  # padding rows untouched
