@@ -653,24 +653,18 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
   const int D = H * dh;
   const float scale = 0.125f;  // 1 / sqrt(64)
   const float* base = qkv + (size_t)b * N * C * (3 * D) + h * dh + lane;
-  float pq[N], pk[N], pv[N];
+  // channel c's q|k|v rows: prefetched from memory into registers one channel ahead, or
+  // (FEAT) formed from the features only when committed to LDS
+  constexpr int NP = FEAT ? 1 : N;
+  float pq[NP], pk[NP], pv[NP];
   FeatW fw;
-  float4 gi[N];
-  if constexpr (FEAT) {
-    fw.load(W0qkv, bqkv, D, h * dh + lane);
-#pragma unroll
-    for (int i = 0; i < N; ++i) gi[i] = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
-  }
+  if constexpr (FEAT) fw.load(W0qkv, bqkv, D, h * dh + lane);
+  int pending = 0;  // channel held by the prefetch registers / to be formed (FEAT)
   auto prefetch = [&](int c) {
+    pending = c;
+    if constexpr (!FEAT) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      if constexpr (FEAT) {
-        const float4 f = feature_channel<T>(c, i, gi[i], (i < n_up) ? 1.f : -1.f);
-        const bool v = c == 0;
-        pq[i] = FeatW::dot(f, fw.wq) + (v ? fw.bq : 0.f);
-        pk[i] = FeatW::dot(f, fw.wk) + (v ? fw.bk : 0.f);
-        pv[i] = FeatW::dot(f, fw.wv) + (v ? fw.bv : 0.f);
-      } else {
+      for (int i = 0; i < N; ++i) {
         const float* r = base + (size_t)(i * C + c) * (3 * D);
         pq[i] = r[0];
         pk[i] = r[D];
@@ -681,9 +675,18 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
   auto commit = [&](float* qd, float* kd, float* vd) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      qd[i * ld + lane] = pq[i];
-      kd[i * ld + lane] = pk[i];
-      vd[i * ld + lane] = pv[i];
+      if constexpr (FEAT) {
+        const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+        const float4 f = feature_channel<T>(pending, i, g, (i < n_up) ? 1.f : -1.f);
+        const bool v = pending == 0;
+        qd[i * ld + lane] = FeatW::dot(f, fw.wq) + (v ? fw.bq : 0.f);
+        kd[i * ld + lane] = FeatW::dot(f, fw.wk) + (v ? fw.bk : 0.f);
+        vd[i * ld + lane] = FeatW::dot(f, fw.wv) + (v ? fw.bv : 0.f);
+      } else {
+        qd[i * ld + lane] = pq[i];
+        kd[i * ld + lane] = pk[i];
+        vd[i * ld + lane] = pv[i];
+      }
     }
   };
   float* obase = o + (size_t)b * N * C * D + h * dh + lane;
@@ -759,13 +762,27 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
       obase[(size_t)(i * C) * D] = acc;
     }
   }
-  float rOL[N], rQu[3][N], rKu[3][N], rVu[3][N];
+  // running flow sums Qu_k = sum_t alpha_kt q_t (and Ku, Vu), one column per lane.  In the
+  // FEAT form they are not accumulated: tangent t moves only electron t/2's features, so
+  // Qu_k[i] = g_k(i) . Wq with g_k(i) = sum_{t of i} alpha_kt f_t(i) (4-vectors), and
+  // Qu_k[i] . Ku_k[j] = g_k(i)^T (Wq Wk^T) g_k(j) with a 4 x 4 Wq Wk^T per head.
+  constexpr int NU = FEAT ? 1 : N;
+  float rOL[N], rQu[3][NU], rKu[3][NU], rVu[3][NU];
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    rOL[i] = 0.f;
+  for (int i = 0; i < N; ++i) rOL[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
 #pragma unroll
     for (int k = 0; k < 3; ++k) rQu[k][i] = rKu[k][i] = rVu[k][i] = 0.f;
-  }
+  // g_k(i) of the FEAT form: alpha-weighted tangent features of electron i
+  auto gflow = [&](int k, int i) -> float4 {
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    const float st = g.x, ct = g.y, sp = g.z, cp = g.w;
+    const float ae = (k == 0) ? -sp : (k == 1 ? cp : 0.f);                  // alpha[k][2i]
+    const float ao = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);  // alpha[k][2i+1]
+    // ae * (-st, ct cp, ct sp, 0) + ao * (0, -sp, cp, 0)
+    return make_float4(-ae * st, ae * ct * cp - ao * sp, ae * ct * sp + ao * cp, 0.f);
+  };
 
   for (int c = 1; c < C; ++c) {
     wsync();
@@ -844,15 +861,17 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
           if (tang) acc2 = fmaf(r, vcr[j], acc2);
         }
         if (tang) {
-          const int t = c - 1;
           rOL[i] = fmaf(2.f, acc2, rOL[i]);
-          const float qv = qc[i * ld + lane], kv = kc[i * ld + lane];
+          if constexpr (!FEAT) {
+            const int t = c - 1;
+            const float qv = qc[i * ld + lane], kv = kc[i * ld + lane];
 #pragma unroll
-          for (int kk = 0; kk < 3; ++kk) {
-            const float a = al[kk * T + t];
-            rQu[kk][i] = fmaf(a, qv, rQu[kk][i]);
-            rKu[kk][i] = fmaf(a, kv, rKu[kk][i]);
-            rVu[kk][i] = fmaf(a, vcr[i], rVu[kk][i]);
+            for (int kk = 0; kk < 3; ++kk) {
+              const float a = al[kk * T + t];
+              rQu[kk][i] = fmaf(a, qv, rQu[kk][i]);
+              rKu[kk][i] = fmaf(a, kv, rKu[kk][i]);
+              rVu[kk][i] = fmaf(a, vcr[i], rVu[kk][i]);
+            }
           }
         } else if (k < 0) {
           acc += rOL[i];
@@ -860,8 +879,13 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
           float a2 = 0.f;
 #pragma unroll
           for (int j = 0; j < N; ++j) {
-            // rVu[k][j] with a runtime k: select without dynamic register indexing
-            const float vu = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
+            float vu;
+            if constexpr (FEAT) {
+              vu = FeatW::dot(gflow(k, j), fw.wv);
+            } else {
+              // rVu[k][j] with a runtime k: select without dynamic register indexing
+              vu = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
+            }
             a2 = fmaf(Au[k * nn + i * N + j], vu, a2);
           }
           acc = fmaf(2.f, a2, acc);
@@ -869,16 +893,38 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
         obase[(size_t)(i * C + c) * D] = acc;
       }
     }
-    if (c == T) {  // last tangent: qu_k . ku_k^T for the flow channels (wave reductions)
+    if (c == T) {  // last tangent: qu_k . ku_k^T for the flow channels
+      if constexpr (FEAT) {
+        // 4 x 4 Wq Wk^T of this head (wave reductions over the head's 64 columns)
+        const float wq[4] = {fw.wq.x, fw.wq.y, fw.wq.z, fw.wq.w};
+        const float wk[4] = {fw.wk.x, fw.wk.y, fw.wk.z, fw.wk.w};
+        float Mqk[4][4];
 #pragma unroll
-      for (int kk = 0; kk < 3; ++kk)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int i = 0; i < N; ++i)
+          for (int e = 0; e < 4; ++e) Mqk[a][e] = wave_sum(wq[a] * wk[e]);
+        for (int p = lane; p < 3 * nn; p += 64) {
+          const int kk = p / nn, pair = p - kk * nn, i = pair / N, j = pair - (pair / N) * N;
+          const float4 gi_ = gflow(kk, i), gj = gflow(kk, j);
+          const float gia[4] = {gi_.x, gi_.y, gi_.z, gi_.w}, gja[4] = {gj.x, gj.y, gj.z, gj.w};
+          float v = 0.f;
 #pragma unroll
-          for (int j = 0; j < N; ++j) {
-            const float v = wave_sum(rQu[kk][i] * rKu[kk][j]);
-            if (lane == 0) QK[kk * nn + i * N + j] = v;
-          }
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v = fmaf(gia[a] * Mqk[a][e], gja[e], v);
+          QK[p] = v;
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+          for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+              const float v = wave_sum(rQu[kk][i] * rKu[kk][j]);
+              if (lane == 0) QK[kk * nn + i * N + j] = v;
+            }
+      }
     }
   }
 }

@@ -837,15 +837,19 @@ void set_gemm_variant(int v) { g_variant = v; }
 void launch_gemm_nt(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* R, int ldr,
                     float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   // measured on MI355X (tools/gemm_bench.py, K = 256): channel rows (>= 64K) take
-  // 128x128 tiles of 32x64 waves when N is a multiple of 256, else 64x64 tiles;
-  // log-psi rows take 64x128 tiles at N = 256 and 64x64 tiles otherwise.
+  // 128x128 tiles of 32x64 waves when N is a multiple of 256 (persistent with a
+  // residual), else 64x64 tiles; log-psi rows take persistent 64x128 tiles for the wide
+  // q|k|v map, 64x128 tiles at N = 256 and 64x64 tiles otherwise.
+  // Persistent variants write whole tiles (rows padded to 256 by every caller; columns
+  // need ldy >= round_up(ncols, 128)).
   int v;
+  const bool pad_ok = ldy >= round_up(ncols, 128);
   if (g_variant >= 100) {
     v = g_variant - 100;
   } else if (rows >= 65536) {
-    v = (ncols % 256 == 0) ? 6 : 7;
+    v = (ncols % 256 == 0) ? ((R && pad_ok) ? 20 : 6) : 7;
   } else {
-    v = (ncols == 256) ? 4 : 7;
+    v = (ncols >= 512 && pad_ok) ? 25 : (ncols == 256 ? 4 : 7);
   }
   launch_gemm_nt_variant(v, X, ldx, Wt, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
 }
