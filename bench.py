@@ -169,6 +169,14 @@ def main():
                 "ms_per_step": ms / args.steps,
                 "avg_us": 1e3 * ms / cnt,
             }
+    # HBM traffic per GEMM launch: rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes)
+    # of this same workload, committed by tools/profile_round.sh; only for the default config
+    traffic = traffic_src = None
+    tf = ROOT / "profiles" / "gemm_traffic.json"
+    if tf.exists() and (B, tuple(args.nspins), args.flux, steps) == (4096, (6, 0), 15, 10):
+        tj = json.loads(tf.read_text())
+        traffic = tj.get("gemm_bytes_per_launch")
+        traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})"
     # dominant kernel: gemm_nt_kernel, all its launches in the instrumented region (log-psi
     # and local-energy GEMMs; classes 0 and 7 of dh_profile_read)
     ig = kinds.index("gemm_ch")
@@ -181,11 +189,13 @@ def main():
         "peak": PEAK_F32_MFMA_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
-        "traffic": None,
+        "traffic": traffic,
         "flops_per_launch": g_fl / g_cnt if g_cnt else 0,
         "avg_launch_us": 1e3 * g_ms / g_cnt if g_cnt else 0,
         "gemm_share_of_step": round(g_ms / (dt_prof * 1e3), 4) if g_ms else None,
         "measured_over": f"{args.steps} instrumented VMC steps (HIP event pair per launch)",
+        "traffic_source": traffic_src,
+        "bytes_per_launch_algorithmic": g_by / g_cnt if g_cnt else 0,
     } if not args.no_kernel_events else None
     B_total = B * world
     value = B_total * args.steps / dt

@@ -6,7 +6,7 @@ import sys
 
 
 def short(name):
-    m = re.search(r"dh::\(anonymous namespace\)::(\w+)", name)
+    m = re.search(r"dh::\(anonymous namespace\)::(\w+(<[^>]*>)?)", name)
     if m:
         return m.group(1)
     if name.startswith("Cijk"):
