@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-components", action="store_true",
                     help="skip the MCMC-only / E_L-only timings (used under rocprofv3 so that every "
                     "profiled GEMM launch belongs to a warmup or timed VMC step)")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="walker groups run on parallel HIP streams within one VMC iteration")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="do not record per-kernel HIP events in the timed region (no roofline)")
     return ap.parse_args()
@@ -70,7 +72,7 @@ def main():
     from deephall_amd.networks import make_network
     from deephall_amd.networks.psiformer import get_handle
     from deephall_amd.random import Key, PRNGKey
-    from deephall_amd.train import init_guess
+    from deephall_amd.train import init_guess, make_vmc_iteration
 
     lib = _lib.load()
     system = config.System(nspins=tuple(args.nspins), flux=args.flux)
@@ -84,10 +86,12 @@ def main():
     key = PRNGKey(7)
     width = 0.1
 
-    def vmc_step(data, key):
-        data, _ = mcmc_step(params, data, key, width, reduce=False)
-        e_l, obs = _run_local_energy(model, params, data)
-        local_stats = device_stats(model, e_l, obs, mcmc_step.last_n_accept, steps)
+    iteration = make_vmc_iteration(model, B, steps, args.groups)
+    iteration1 = make_vmc_iteration(model, B, steps, 1)  # instrumented region: one stream
+
+    def vmc_step(data, key, it=iteration):
+        data, e_l, obs, n_accept = it(params, data, key, width)
+        local_stats = device_stats(model, e_l, obs, n_accept, steps)
         stats = reduce_stats(local_stats)  # the one all-reduce of the step
         return data, stats
 
@@ -122,7 +126,8 @@ def main():
     # ---------------- instrumented region: the same K steps again with a HIP event pair
     # around every kernel launch (on the launch stream), for the per-kernel breakdown and
     # the roofline.  The events themselves cost ~10 % of a step, so `value` comes from the
-    # un-instrumented region above.
+    # un-instrumented region above; the walker groups run one after the other here so
+    # that each launch's duration is its own.
     import ctypes as C
 
     prof = (C.c_double * (4 * len(_lib.PROF_KINDS)))()
@@ -132,7 +137,7 @@ def main():
         barrier()
         a = time.perf_counter()
         for _ in range(args.steps):
-            data, _ = vmc_step(data, key)
+            data, _ = vmc_step(data, key, iteration1)  # kernels one at a time: clean durations
             key = key.advance(steps)
         barrier()
         dt_prof = time.perf_counter() - a
@@ -219,6 +224,7 @@ def main():
             "walkers_per_gpu": B,
             "global_batch": B_total,
             "parallelism": f"walker-dp{world}",
+            "walker_groups_per_gpu": args.groups,
         },
         "walker_steps_per_sec": round(value * steps, 1),
         "components": {

@@ -93,7 +93,7 @@ class NativeHandle:
         self.lib.dh_param_layout(self.h, offs, nseg + 1)
         self.offsets = [int(o) for o in offs]
         self.nparams = self.offsets[-1]
-        self.ws = None
+        self.ws = {}  # one workspace per HIP stream (walker groups may run on parallel streams)
         self._params_key = None
 
     def __del__(self):
@@ -104,11 +104,15 @@ class NativeHandle:
             pass
 
     def workspace(self, nbytes: int) -> torch.Tensor:
-        if self.ws is None or self.ws.numel() < nbytes:
-            self.ws = None
+        sid = torch.cuda.current_stream(self.device).cuda_stream
+        ws = self.ws.get(sid)
+        if ws is None or ws.numel() < nbytes:
+            self.ws.pop(sid, None)
+            ws = None
             torch.cuda.empty_cache()
-            self.ws = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
-        return self.ws
+            ws = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self.ws[sid] = ws
+        return ws
 
     def set_params(self, packed: torch.Tensor, key):
         if self._params_key == key:

@@ -83,7 +83,57 @@ def setup_mcmc(cfg: Config, model):
     return step, pmoves
 
 
-def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | None = None):
+def make_vmc_iteration(model, batch_per_device: int, steps: int, groups: int = 2):
+    """The device work of one VMC iteration (train.py:128-140 before the statistics):
+    ``mcmc_step`` then the local energy, for this rank's walkers.
+
+    The walkers are independent and the device RNG is keyed by global walker index, so
+    the batch is cut into ``groups`` contiguous walker groups, each run start to finish
+    (its MCMC moves, then its local energies) on its own HIP stream; the results are
+    bit-identical to one group (same walkers, same random numbers, same arithmetic).
+    Measured on MI355X at C2 (4096 walkers): 2 groups 12.8 ms vs 1 group 10.75 ms per
+    iteration — co-scheduled kernels of two groups slow each other down more than they
+    fill idle CUs — so the default is one group; the option stays for smaller kernels.
+
+    Returns ``iteration(params, data, key, width) -> (data, e_l [B,2], obs [B,8],
+    n_accept [B])``; data is updated in place.
+    """
+    B = batch_per_device
+    groups = max(1, min(int(groups), B))
+    sizes = [B // groups + (1 if g < B % groups else 0) for g in range(groups)]
+    mcmc = [make_mcmc_step(model, n, steps) for n in sizes]
+    side: list = []
+
+    def iteration(params, data: torch.Tensor, key, width):
+        main = torch.cuda.current_stream(data.device)
+        while len(side) < groups - 1:
+            side.append(torch.cuda.Stream(data.device))
+        base = constants.rank() * B
+        outs, off = [], 0
+        for g, n in enumerate(sizes):
+            s = main if g == 0 else side[g - 1]
+            if g > 0:
+                s.wait_stream(main)
+            with torch.cuda.stream(s):
+                d = data[off : off + n]
+                mcmc[g](params, d, key, width, reduce=False, walker_offset=base + off)
+                e, o = _run_local_energy(model, params, d)
+                outs.append((e, o, mcmc[g].last_n_accept))
+            off += n
+        for s in side[: groups - 1]:
+            main.wait_stream(s)
+        for g in range(1, groups):
+            for t in outs[g]:
+                t.record_stream(main)
+        if groups == 1:
+            return data, outs[0][0], outs[0][1], outs[0][2]
+        return data, torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs]), torch.cat([o[2] for o in outs])
+
+    iteration.sizes = sizes
+    return iteration
+
+
+def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | None = None, groups: int = 1):
     """Inference-mode VMC loop (optimizer 'none').  Returns the list of per-iteration stats."""
     init_distributed()
     model = make_network(cfg.system, cfg.network)
@@ -96,11 +146,11 @@ def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | Non
         key = key.advance(steps)
     history = []
     iters = cfg.optim.iterations if iterations is None else iterations
+    iteration = make_vmc_iteration(model, data.shape[0], steps, groups)
     for t in range(iters):
-        data, _ = mcmc_step(params, data, key, width, reduce=False)
+        data, e_l, obs, n_accept = iteration(params, data, key, width)
         key = key.advance(steps)
-        e_l, obs = _run_local_energy(model, params, data)
-        local = device_stats(model, e_l, obs, mcmc_step.last_n_accept, steps)
+        local = device_stats(model, e_l, obs, n_accept, steps)
         stats = reduce_stats(local)  # the single all-reduce of this iteration
         width, pmoves = update_mcmc_width(t, width, cfg.mcmc.adapt_frequency, stats["pmove"], pmoves)
         row = {k: (complex(v.item()) if v.is_complex() else float(v.item())) for k, v in stats.items()}

@@ -243,11 +243,11 @@ def test_mcmc_sharding_invariance(cuda):
     assert torch.equal(xa, torch.cat([x0, x1]))
 
 
-def test_energy_stats_kernel(cuda):
+@pytest.mark.parametrize("B", [1000, 4096, 20000])  # 20000: the one-part-at-a-time sort path
+def test_energy_stats_kernel(cuda, B):
     ocfg = oracle_config("C1")
     system, model = build(ocfg)
-    g = np.random.default_rng(0)
-    B = 1000
+    g = np.random.default_rng(B)
     e = g.standard_normal((B, 2)).astype(np.float32)
     e[:, 0] += 3.0
     e[7, 0] = 1e6  # outlier gets clipped
@@ -268,3 +268,27 @@ def test_energy_stats_kernel(cuda):
     assert out[5] == pytest.approx(obs[:, 0].mean(), abs=1e-5)
     assert out[11] == pytest.approx(nacc.sum() / (10 * B), rel=1e-6)
     assert out[12] == B - 1
+
+
+def test_walker_groups_on_parallel_streams_are_bit_identical(cuda):
+    """make_vmc_iteration with 2 / 3 walker groups on parallel HIP streams == 1 group."""
+    from deephall_amd.random import PRNGKey
+    from deephall_amd.train import make_vmc_iteration
+
+    ocfg = oracle_config("C2")
+    system, model = build(ocfg)
+    params = model.init(PRNGKey(3), device=cuda)
+    B = 96
+    x0 = init_guess(Key(11), B, sum(ocfg.nspins), cuda, network=model)
+    ref = None
+    for groups in (1, 2, 3):
+        it = make_vmc_iteration(model, B, 4, groups)
+        x = x0.clone()
+        x, e, o, n = it(params, x, Key(5), 0.2)
+        torch.cuda.synchronize()
+        got = (x.cpu(), e.cpu(), o.cpu(), n.cpu())
+        if ref is None:
+            ref = got
+        else:
+            for a, b in zip(ref, got):
+                assert torch.equal(a, b), groups
