@@ -20,6 +20,9 @@ LIB = OUT_DIR / "libdeephall_amd.so"
 ARCH = os.environ.get("DH_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I", str(ROOT / "include")]
+# per-file extras: the split-bf16 GEMM keeps its f32 subtractions scalar (packed f32 VALU
+# between MFMAs costs more issue cycles than it saves, MI355X_MICROARCH.md cycle table)
+EXTRA = {"gemm_x6.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():
@@ -38,7 +41,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
         objs.append(obj)
         if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
             continue
-        cmd = [HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *FLAGS, *EXTRA.get(src.name, []), "-c", str(src), "-o", str(obj)]
         if src.suffix == ".cpp":
             cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
         if verbose:

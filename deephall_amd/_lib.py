@@ -36,6 +36,7 @@ EXPORTS = [
     "dh_param_layout",
     "dh_set_params",
     "dh_workspace_bytes",
+    "dh_set_gemm_mode",
     "dh_logpsi",
     "dh_mcmc_step",
     "dh_local_energy",
@@ -45,6 +46,9 @@ EXPORTS = [
     "dh_debug_trunk",
     "dh_debug_gemm",
     "dh_debug_gemm_ln",
+    "dh_debug_x6_plane_rows",
+    "dh_debug_split_planes",
+    "dh_debug_gemm_x6",
     "dh_profile_enable",
     "dh_profile_read",
     "dh_debug_f_offset",
@@ -99,6 +103,8 @@ def load(path: Path | str | None = None):
     lib.dh_set_params.restype = i32
     lib.dh_workspace_bytes.argtypes = [vp, i32, i32]
     lib.dh_workspace_bytes.restype = sz
+    lib.dh_set_gemm_mode.argtypes = [vp, i32]
+    lib.dh_set_gemm_mode.restype = i32
     lib.dh_logpsi.argtypes = [vp, vp, i32, vp, vp, sz, vp]
     lib.dh_logpsi.restype = i32
     lib.dh_mcmc_step.argtypes = [vp, vp, vp, vp, i32, i32, C.c_float, u64, u64, i64, vp, vp, sz, vp]
@@ -119,6 +125,12 @@ def load(path: Path | str | None = None):
     lib.dh_debug_gemm.restype = i32
     lib.dh_debug_gemm_ln.argtypes = [i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp]
     lib.dh_debug_gemm_ln.restype = i32
+    lib.dh_debug_x6_plane_rows.argtypes = [i32]
+    lib.dh_debug_x6_plane_rows.restype = i32
+    lib.dh_debug_split_planes.argtypes = [vp, i32, i32, i32, vp, vp]
+    lib.dh_debug_split_planes.restype = i32
+    lib.dh_debug_gemm_x6.argtypes = [i32, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp]
+    lib.dh_debug_gemm_x6.restype = i32
     lib.dh_profile_enable.argtypes = [vp, i32]
     lib.dh_profile_enable.restype = i32
     lib.dh_profile_read.argtypes = [vp, C.POINTER(C.c_double), i32]

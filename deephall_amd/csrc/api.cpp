@@ -97,6 +97,8 @@ struct dh_handle {
   float* params = nullptr;
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
   float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
+  uint16_t* wp = nullptr;  // split-bf16 weight planes for the x6 kernels (device)
+  int gemm_mode = DH_GEMM_X6;
   std::vector<float> norm_host;
   bool params_set = false;
   Profiler prof;
@@ -214,6 +216,7 @@ void dh_destroy(dh_handle* h) {
   if (h->params) (void)hipFree(h->params);
   if (h->norm) (void)hipFree(h->norm);
   if (h->wt) (void)hipFree(h->wt);
+  if (h->wp) (void)hipFree(h->wp);
   delete h;
 }
 
@@ -277,9 +280,36 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
     }
     launch_transpose(h->p.Worb, d.ld_orb, D, d.orb_cols, q, D, st);
     h->p.WorbT = q;
+    // split-bf16 planes of the same weights (gemm_x6.hip), from the transposed copies
+    const size_t pq = (size_t)3 * x6_plane_rows(3 * D) * D, pd = (size_t)3 * x6_plane_rows(D) * D;
+    const size_t po = (size_t)3 * x6_plane_rows(d.orb_cols) * D;
+    const size_t ptotal = (size_t)d.L * (pq + 2 * pd) + po;
+    if (!h->wp) HIP_TRY(hipMalloc(&h->wp, ptotal * sizeof(uint16_t)));
+    uint16_t* w = h->wp;
+    for (int l = 0; l < d.L; ++l) {
+      LayerParams& lp = h->p.layer[l];
+      launch_split_planes(lp.WqkvT, D, 3 * D, D, w, st);
+      lp.WqkvP = w;
+      w += pq;
+      launch_split_planes(lp.WolT, D, D, D, w, st);
+      lp.WolP = w;
+      w += pd;
+      launch_split_planes(lp.WmT, D, D, D, w, st);
+      lp.WmP = w;
+      w += pd;
+    }
+    launch_split_planes(h->p.WorbT, D, d.orb_cols, D, w, st);
+    h->p.WorbP = w;
     HIP_TRY(hipGetLastError());
   }
   h->params_set = true;
+  return DH_OK;
+}
+
+int dh_set_gemm_mode(dh_handle* h, int mode) {
+  if (!h) return fail(DH_EINVAL, "null handle");
+  if (mode != DH_GEMM_F32 && mode != DH_GEMM_X6) return fail(DH_EINVAL, "bad GEMM mode");
+  h->gemm_mode = mode;
   return DH_OK;
 }
 
@@ -301,10 +331,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const double R = rows, DD = D, f4 = 4.0;
   const bool nt = P.WorbT != nullptr;
   const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
-  auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, int ldw, const float* bias,
-                  const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
+  // channel rows (local energy) take the split-bf16 GEMM unless exact-f32 is requested
+  const bool x6 = nt && C > 1 && h->gemm_mode == DH_GEMM_X6 && gemm_x6_supported(D);
+  auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, const uint16_t* Wp, int ldw,
+                  const float* bias, const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
     PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
-    if (nt)
+    if (x6)
+      launch_gemm_x6(X, ldx, Wp, x6_plane_rows(ncols), bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
+    else if (nt)
       launch_gemm_nt(X, ldx, Wt, K, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
     else
       launch_gemm(X, ldx, W, ldw, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
@@ -321,7 +355,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0) gemm(w.h, D, lp.Wqkv, lp.WqkvT, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    if (l > 0) gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
@@ -340,18 +374,18 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       continue;
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
-    gemm(w.o, D, lp.Wol, lp.WolT, D, lp.bol, w.h, D, w.t, D, D, D);
+    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, w.h, D, w.t, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
       launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
     }
-    gemm(w.h, D, lp.Wm, lp.WmT, D, lp.bm, nullptr, 0, w.o, D, D, D);
+    gemm(w.h, D, lp.Wm, lp.WmT, lp.WmP, D, lp.bm, nullptr, 0, w.o, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 3.0 * DD);
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  gemm(w.h, D, P.Worb, P.WorbT, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
+  gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
 
@@ -479,6 +513,25 @@ int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw,
     launch_gemm_variant(variant < 0 ? 0 : variant, X, ldx, W, ldw, bias, R, ldr, Y, ldy, rows, ncols, K, C,
                         (hipStream_t)stream);
   }
+  return check_launch();
+}
+
+int dh_debug_x6_plane_rows(int ncols) { return x6_plane_rows(ncols); }
+
+int dh_debug_split_planes(const float* Wt, int ldw, int ncols, int K, uint16_t* Wp, void* stream) {
+  if (!Wt || !Wp || ncols < 1 || K < 1) return fail(DH_EINVAL, "bad split_planes args");
+  launch_split_planes(Wt, ldw, ncols, K, Wp, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_debug_gemm_x6(int variant, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                     const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream) {
+  if (!gemm_x6_supported(K) || ldp < x6_plane_rows(ncols)) return fail(DH_EINVAL, "bad gemm_x6 args");
+  if (variant >= 10 && K > 256) return fail(DH_EINVAL, "persistent gemm_x6 needs K <= 256");
+  if (variant < 0)
+    launch_gemm_x6(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, (hipStream_t)stream);
+  else
+    launch_gemm_x6_variant(variant, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, (hipStream_t)stream);
   return check_launch();
 }
 

@@ -28,6 +28,7 @@ struct Dims {
 struct LayerParams {
   const float *Wqkv, *bqkv, *Wol, *bol, *ln1, *Wm, *bm, *ln2;
   const float *WqkvT, *WolT, *WmT;  // transposed copies [ncols pad 256][D] for the NT GEMM
+  const uint16_t *WqkvP, *WolP, *WmP;  // split-bf16 planes [3][x6_plane_rows(ncols)][D] (gemm_x6)
 };
 struct Params {
   const float* W0;
@@ -35,6 +36,7 @@ struct Params {
   const float *Worb, *borb, *jastrow;
   const float* W0qkv;  // [4][3D] = W0 @ Wqkv of layer 0 (folded on the host)
   const float* WorbT;  // [orb_cols pad 256][D]
+  const uint16_t* WorbP;  // split-bf16 planes of Worb
 };
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
@@ -75,6 +77,17 @@ void launch_gemm_nt(const float* X, int ldx, const float* Wt, int ldw, const flo
 bool gemm_ln_supported(int D, int K);
 void launch_gemm_ln(const float* X, int ldx, const float* Wt, int ldw, const float* bias, const float* ln, float* h,
                     int rows, int K, int mode, int bm, hipStream_t s);
+// gemm_x6.hip: split-bf16 GEMM (f32-accurate, 6 bf16 MFMAs per product block).
+// Wp = three bf16 planes [3][ldp][K] of the transposed weight (launch_split_planes),
+// ldp = x6_plane_rows(ncols); K % 32 == 0; X holds round_up(rows, 256) readable rows.
+int x6_plane_rows(int ncols);
+void launch_split_planes(const float* Wt, int ldw, int ncols, int K, uint16_t* Wp, hipStream_t s);
+bool gemm_x6_supported(int K);
+void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
+                            hipStream_t s);
+void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).
 void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s);
 

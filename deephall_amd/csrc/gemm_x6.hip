@@ -1,0 +1,1420 @@
+// Split-bf16 GEMM ("x6") on CDNA4 matrix cores: f32-accurate products at bf16 MFMA rate.
+//
+//   Y[r][n] = sum_k X[r][k] W[k][n]  + (r % C == 0 ? bias[n] : 0)  + (R ? R[r][n] : 0)
+//
+// Same contract as gemm_nt_kernel (gemm.hip); used for the channel rows of the local
+// energy (all 2N+5 channels of every linear map, psiformer.py:42-47, blocks.py:29-35).
+//
+// Numerics.  Every f32 operand is split exactly into three bf16 terms, a = a0 + a1 + a2
+// (round-to-nearest at each step: a0 = bf16(a), a1 = bf16(a - a0), a2 = a - a0 - a1,
+// which has at most 8 significant bits and is therefore exact in bf16), with
+// |a1| <= 2^-8 |a|, |a2| <= 2^-16 |a|.  The product is formed from the six terms
+// larger than 2^-24 |a b|:
+//     a b ~= a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)
+// The three dropped terms (a1 b2, a2 b1, a2 b2) are <= 2^-24 |a b| together, i.e. at
+// the f32 unit roundoff; v_mfma_f32_32x32x16_bf16 multiplies bf16 exactly and
+// accumulates in f32, so the result carries the error of an f32 GEMM (measured in
+// tests/test_gpu_kernels.py against float64 next to the f32-MFMA kernel).  Cost: 6 bf16
+// MFMAs (6 x 32 cycles) per 32x32x16 block against 8 f32 MFMAs (8 x 64 cycles):
+// 2.67x the f32 matrix rate at equal accuracy.
+//
+// Operands.  The weight is split once per dh_set_params into three bf16 planes
+// Wp[p][n][k] (n padded; launch_split_planes).  The activation tile is staged as f32
+// by LDS-DMA (as gemm_nt_kernel: 128-B rows, 16-B slots XOR-swizzled by (row>>1)&7) and
+// split in registers by the one wave that consumes it: wave w owns rows 32w..32w+31 of
+// the tile and all BN = 32*TN columns, so every activation element is split exactly
+// once.  B planes are staged by LDS-DMA into [plane][BN][64 B] images, 16-B slots
+// swizzled by (row>>2)&3 (16 lanes of a ds_read_b128 pass hit 16 distinct bank groups).
+#include "dh_internal.h"
+#include "device_common.h"
+
+namespace dh {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int X6_BK = 32;  // k per LDS stage (two 16-k MFMA chunks)
+
+int cu_count_x6() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+// two f32 -> packed bf16 pair (one v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
+}
+__device__ __forceinline__ float lo_f(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_f(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// 8 f32 -> three bf16x8 terms (per pair: 3 v_cvt_pk_bf16_f32, 4 unpacks, 4 v_sub_f32)
+__device__ __forceinline__ void split3(const float4& u, const float4& v, bf16x8& h, bf16x8& m, bf16x8& l) {
+  const float a[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  u32x4v H, Mv, Lv;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float x = a[2 * p], y = a[2 * p + 1];
+    const uint32_t h2 = pk_bf16(x, y);
+    const float rx = x - lo_f(h2), ry = y - hi_f(h2);
+    const uint32_t m2 = pk_bf16(rx, ry);
+    const float sx = rx - lo_f(m2), sy = ry - hi_f(m2);
+    H[p] = h2;
+    Mv[p] = m2;
+    Lv[p] = pk_bf16(sx, sy);
+  }
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, Mv);
+  l = __builtin_bit_cast(bf16x8, Lv);
+}
+
+// One wave = 32 rows x (32*TN) columns; NW waves stacked along rows (BM = 32*NW).
+template <int NW, int TN, bool HAS_R>
+__global__ __launch_bounds__(NW * 64) void gemm_x6_kernel(const float* __restrict__ X, int ldx,
+                                                          const uint16_t* __restrict__ Wp, int ldp,
+                                                          const float* __restrict__ bias, const float* R, int ldr,
+                                                          float* Y, int ldy, int rows, int ncols, int K, int C,
+                                                          int ntm, int ntn) {
+  constexpr int BM = 32 * NW, BN = 32 * TN, BK = X6_BK;
+  constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int IA = BM / 8, IBP = BN / 16, IB = 3 * IBP;  // DMA wave-instructions (1 KiB each)
+  constexpr int PER = (IA + IB + NW - 1) / NW;
+  constexpr bool PREF = HAS_R && TN <= 4;  // residual prefetched into registers (wider tiles would spill)
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+
+  // XCD-aware tile order (as gemm_nt_kernel): consecutive tiles of a row panel share an XCD
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const size_t plane = (size_t)ldp * K;  // elements per weight plane
+
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto stage = [&](int k0, int buf) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int j = wid + t * NW;  // wave-uniform
+      if ((IA + IB) % NW != 0 && j >= IA + IB) break;
+      const void* src;
+      uint32_t dst;
+      if (j < IA) {  // 8 rows x 128 B of f32 activations
+        const int r = j * 8 + (lane >> 3);
+        const int sl = ((lane & 7) ^ ((r >> 1) & 7)) * 4;
+        src = X + (size_t)(row0 + r) * ldx + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + j * 8 * BK * 4);
+      } else {  // 16 rows x 64 B of one bf16 weight plane
+        const int jb = j - IA, p = jb / IBP, rg = (jb % IBP) * 16;
+        const int r = rg + (lane >> 2);
+        const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 8;
+        src = Wp + p * plane + (size_t)(col0 + r) * K + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + A_BYTES + p * B_PLANE + rg * BK * 2);
+      }
+      dst = __builtin_amdgcn_readfirstlane(dst);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  };
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+  float rres[PREF ? TN : 1][16];
+
+  const int nk = K / BK;
+  stage(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) stage((kt + 1) * BK, cur ^ 1);
+    if (PREF && kt + 1 == nk) {  // residual loads overlap the last k-tile's MFMAs
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int c = col0 + ni * 32 + l32;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = row0 + wid * 32 + 4 * lh + (e & 3) + 8 * (e >> 2);
+          rres[ni][e] = (c < ncols && r < rows) ? R[(size_t)r * ldr + c] : 0.f;
+        }
+      }
+    }
+    const char* As = smem + cur * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ch = 0; ch < BK / 16; ++ch) {
+      // A fragment: row m, k = 16 ch + 8 lh + (0..7) = logical slots 4ch + 2lh, +1
+      const int m = wid * 32 + l32;
+      const int s0 = 4 * ch + 2 * lh;
+      const float* arow = reinterpret_cast<const float*>(As) + m * BK;
+      const float4 u = *reinterpret_cast<const float4*>(arow + ((s0 ^ ((m >> 1) & 7)) * 4));
+      const float4 v = *reinterpret_cast<const float4*>(arow + (((s0 + 1) ^ ((m >> 1) & 7)) * 4));
+      bf16x8 a0, a1, a2;
+      split3(u, v, a0, a1, a2);
+      const int sb = 2 * ch + lh;  // B fragment: k = 16 ch + 8 lh + (0..7) = slot sb of a 64-B row
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = j * 32 + l32;
+        const int off = n * BK * 2 + ((sb ^ ((n >> 2) & 3)) * 16);
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bs + off);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + off);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + off);
+        // smallest terms first
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[j], 0, 0, 0);
+      }
+    }
+  }
+
+  // Epilogue. C/D map of 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+  const int rbase = row0 + wid * 32 + 4 * lh;
+  const int rm0 = (C == 1) ? 0 : rbase % C;
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int c = col0 + ni * 32 + l32;
+    if (c >= ncols) continue;
+    const float bv = bias ? bias[c] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int off = (e & 3) + 8 * (e >> 2);
+      const int r = rbase + off;
+      if (r >= rows) continue;
+      float v = acc[ni][e];
+      if (bias) {
+        bool val = true;
+        if (C > 1) {
+          int t = rm0 + off;
+          while (t >= C) t -= C;
+          val = (t == 0);
+        }
+        if (val) v += bv;
+      }
+      if (PREF) v += rres[PREF ? ni : 0][e];
+      else if (HAS_R) v += R[(size_t)r * ldr + c];
+      Y[(size_t)r * ldy + c] = v;
+    }
+  }
+}
+
+template <int NW, int TN>
+void launch_x6_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                 float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  constexpr int BM = 32 * NW, BN = 32 * TN;
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  const size_t smem = 2ull * (BM * X6_BK * 4 + 3 * BN * X6_BK * 2);
+  if (R) {
+    ensure_smem(gemm_x6_kernel<NW, TN, true>, smem);
+    hipLaunchKernelGGL((gemm_x6_kernel<NW, TN, true>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp, ldp, bias,
+                       R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+  } else {
+    ensure_smem(gemm_x6_kernel<NW, TN, false>, smem);
+    hipLaunchKernelGGL((gemm_x6_kernel<NW, TN, false>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp, ldp,
+                       bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+  }
+}
+
+// ---- big-tile form: 256 x (64*TN) tiles, 4 x 2 waves of 64 x 32*TN, BK = 16, DMA ring ----
+// Intensity: per 16-k step a workgroup moves 256 x 64 B of A (f32) + BN x 96 B of B (three
+// planes) for 2 x 256 x BN x 16 flops: 51 flop/B at BN = 256 (the 64-row tiles above move
+// 2x the bytes per flop, which the L2 -> CU path cannot feed at bf16 MFMA rate).
+// LDS images per stage: A [256][64 B], 16-B slot s of row m at s ^ ((m >> 2) & 3);
+// B [plane][BN][32 B], slot h of row n at h ^ ((n >> 3) & 1)  (conflict-free b128 reads).
+// Every wave issues exactly PER DMA instructions per stage (surplus slots repeat the last
+// piece, an identical write), so the counted vmcnt waits are exact.
+template <int TN, int STAGES>
+__global__ __launch_bounds__(512) void gemm_x6b_kernel(const float* __restrict__ X, int ldx,
+                                                       const uint16_t* __restrict__ Wp, int ldp,
+                                                       const float* __restrict__ bias, const float* R, int ldr,
+                                                       float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
+                                                       int ntn) {
+  constexpr int NW = 8, BM = 256, WN = 32 * TN, BN = 2 * WN, BK = 16;
+  constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int IA = A_BYTES / 1024, IB = 3 * B_PLANE / 1024, PER = (IA + IB + NW - 1) / NW;
+  static_assert(A_BYTES % 1024 == 0 && B_PLANE % 1024 == 0, "DMA pieces");
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int l32 = lane & 31, lh = lane >> 5;
+
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const size_t plane = (size_t)ldp * K;
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+
+  auto stage = [&](int k0, int buf) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      int j = wid + t * NW;
+      if (j >= IA + IB) j = IA + IB - 1;  // wave-uniform: repeat the last piece
+      const void* src;
+      uint32_t dst;
+      if (j < IA) {  // 16 rows x 64 B of f32 activations
+        const int r = j * 16 + (lane >> 2);
+        const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
+        src = X + (size_t)(row0 + r) * ldx + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + j * 1024);
+      } else {  // 32 rows x 32 B of one weight plane
+        const int jb = j - IA, p = jb / (B_PLANE / 1024), rg = (jb % (B_PLANE / 1024)) * 32;
+        const int r = rg + (lane >> 1);
+        const int sl = ((lane & 1) ^ ((r >> 3) & 1)) * 8;
+        src = Wp + p * plane + (size_t)(col0 + r) * K + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + A_BYTES + p * B_PLANE + rg * 32);
+      }
+      dst = __builtin_amdgcn_readfirstlane(dst);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  };
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = K / BK;
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < nk) stage(t * BK, t);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (STAGES == 3 && kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + STAGES - 1 < nk) {
+      int nb = cur + STAGES - 1;
+      if (nb >= STAGES) nb -= STAGES;
+      stage((kt + STAGES - 1) * BK, nb);
+    }
+    const char* As = smem + cur * STAGE;
+    const char* Bs = As + A_BYTES;
+    if (++cur == STAGES) cur = 0;
+    bf16x8 a0[2], a1[2], a2[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // A fragment: row m, k = 8 lh + (0..7) = slots 2lh, 2lh+1
+      const int m = wm * 64 + i * 32 + l32;
+      const float* arow = reinterpret_cast<const float*>(As) + m * BK;
+      const float4 u = *reinterpret_cast<const float4*>(arow + (((2 * lh) ^ ((m >> 2) & 3)) * 4));
+      const float4 v = *reinterpret_cast<const float4*>(arow + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 4));
+      split3(u, v, a0[i], a1[i], a2[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wn * WN + j * 32 + l32;
+      const int off = n * 32 + ((lh ^ ((n >> 3) & 1)) * 16);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bs + off);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + off);
+      const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + off);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[i], b0, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b2, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b0, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b1, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b0, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rbase = row0 + wm * 64 + i * 32 + 4 * lh;
+    const int rm0 = (C == 1) ? 0 : rbase % C;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = col0 + wn * WN + j * 32 + l32;
+      if (c >= ncols) continue;
+      const float bv = bias ? bias[c] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int off = (e & 3) + 8 * (e >> 2);
+        const int r = rbase + off;
+        if (r >= rows) continue;
+        float v = acc[i][j][e];
+        if (bias) {
+          int t = rm0 + off;
+          while (t >= C) t -= C;
+          if (t == 0) v += bv;
+        }
+        if (R) v += R[(size_t)r * ldr + c];
+        Y[(size_t)r * ldy + c] = v;
+      }
+    }
+  }
+}
+
+template <int TN, int STAGES>
+void launch_x6b_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  constexpr int BM = 256, BN = 64 * TN;
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  const size_t smem = (size_t)STAGES * (BM * 16 * 4 + 3 * BN * 16 * 2);
+  ensure_smem(gemm_x6b_kernel<TN, STAGES>, smem);
+  hipLaunchKernelGGL((gemm_x6b_kernel<TN, STAGES>), dim3(ntm * ntn), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R,
+                     ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+}
+
+// ---- pipelined form: 256 x 32*TN tiles, 8 waves of 32 x 32*TN, BK = 16, 3-buffer ring ----
+// The split of the NEXT k-tile's activations runs between the MFMAs of the current one
+// (its f32 fragment is read from LDS one k-tile ahead), so the matrix cores do not idle
+// through a VALU-only phase after every barrier.  Ring: at iteration kt the DMA fills
+// buffer (kt+2)%3 (last read in iteration kt-1, retired by this iteration's barrier), A of
+// kt+1 is read from buffer (kt+1)%3 (landed: vmcnt(0) + barrier), B of kt from kt%3.
+// Every activation element is split by exactly one wave (wave w owns rows 32w..32w+31).
+template <int TN>
+__global__ __launch_bounds__(512) void gemm_x6c_kernel(const float* __restrict__ X, int ldx,
+                                                       const uint16_t* __restrict__ Wp, int ldp,
+                                                       const float* __restrict__ bias, const float* R, int ldr,
+                                                       float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
+                                                       int ntn) {
+  constexpr int NW = 8, BM = 256, BN = 32 * TN, BK = 16;
+  constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE + 1023) / 1024, PER = (IA + IB + NW - 1) / NW;
+  static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const size_t plane = (size_t)ldp * K;
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+
+  auto stage = [&](int k0, int buf) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      int j = wid + t * NW;
+      if (j >= IA + IB) j = IA + IB - 1;  // wave-uniform: repeat the last piece
+      const void* src;
+      uint32_t dst;
+      if (j < IA) {  // 16 rows x 64 B of f32 activations
+        const int r = j * 16 + (lane >> 2);
+        const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
+        src = X + (size_t)(row0 + r) * ldx + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + j * 1024);
+      } else {  // 32 rows x 32 B of the weight planes, rows (plane, n) contiguous
+        const int q = (j - IA) * 32 + (lane >> 1);  // global row of the [3][BN] image
+        const int p = q / BN, n = q % BN;
+        const int sl = ((lane & 1) ^ ((n >> 3) & 1)) * 8;
+        src = Wp + p * plane + (size_t)(col0 + n) * K + k0 + sl;
+        dst = lds0 + (uint32_t)(buf * STAGE + A_BYTES + (j - IA) * 1024);
+      }
+      dst = __builtin_amdgcn_readfirstlane(dst);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  };
+  const int m = wid * 32 + l32;  // this lane's A row within the tile
+  auto read_a = [&](int buf, float4& u, float4& v) {
+    const float* arow = reinterpret_cast<const float*>(smem + buf * STAGE) + m * BK;
+    u = *reinterpret_cast<const float4*>(arow + (((2 * lh) ^ ((m >> 2) & 3)) * 4));
+    v = *reinterpret_cast<const float4*>(arow + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 4));
+  };
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  const int nk = K / BK;
+  stage(0, 0);
+  if (nk > 1) stage(BK, 1);
+  if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bf16x8 c0, c1, c2;  // split fragments of the current k-tile
+  {
+    float4 u, v;
+    read_a(0, u, v);
+    split3(u, v, c0, c1, c2);
+  }
+  int bcur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued one iteration ago)
+    __syncthreads();
+    int bn1 = bcur + 1, bn2 = bcur + 2;
+    if (bn1 >= 3) bn1 -= 3;
+    if (bn2 >= 3) bn2 -= 3;
+    if (kt + 2 < nk) stage((kt + 2) * BK, bn2);
+    const bool more = kt + 1 < nk;
+    float4 u, v;
+    if (more) read_a(bn1, u, v);
+    const char* Bs = smem + bcur * STAGE + A_BYTES;
+    bf16x8 n0, n1, n2;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = j * 32 + l32;
+      const int off = n * 32 + ((lh ^ ((n >> 3) & 1)) * 16);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bs + off);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + off);
+      const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + off);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c2, b0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, b2, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, b1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, b0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, b1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, b0, acc[j], 0, 0, 0);
+      if (j == TN / 2 && more) split3(u, v, n0, n1, n2);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      c0 = n0;
+      c1 = n1;
+      c2 = n2;
+    }
+    bcur = bn1;
+  }
+
+  const int rbase = row0 + wid * 32 + 4 * lh;
+  const int rm0 = (C == 1) ? 0 : rbase % C;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c = col0 + j * 32 + l32;
+    if (c >= ncols) continue;
+    const float bv = bias ? bias[c] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int off = (e & 3) + 8 * (e >> 2);
+      const int r = rbase + off;
+      if (r >= rows) continue;
+      float val = acc[j][e];
+      if (bias) {
+        int t = rm0 + off;
+        while (t >= C) t -= C;
+        if (t == 0) val += bv;
+      }
+      if (R) val += R[(size_t)r * ldr + c];
+      Y[(size_t)r * ldy + c] = val;
+    }
+  }
+}
+
+template <int TN>
+void launch_x6c_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  constexpr int BM = 256, BN = 32 * TN;
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  const size_t smem = 3ull * (BM * 16 * 4 + 3 * BN * 16 * 2);
+  ensure_smem(gemm_x6c_kernel<TN>, smem);
+  hipLaunchKernelGGL((gemm_x6c_kernel<TN>), dim3(ntm * ntn), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
+                     ldy, rows, ncols, K, C, ntm, ntn);
+}
+
+// ---- lean pipelined form (the production kernel) -------------------------------------------
+// As gemm_x6c_kernel (256 x 32*TN tiles, 8 waves of 32 rows, BK = 16, 3-buffer ring, next
+// k-tile's split between the current MFMAs), with the issue budget of a bf16 MFMA in mind
+// (an MFMA gap of 32 cycles holds ~6 VALU issues, MI355X_MICROARCH.md cycle table):
+//  * DMA sources are a per-lane 32-bit offset fixed for the whole tile plus a scalar base
+//    advanced per k-tile (global_load_lds saddr form: no VALU address math in the loop);
+//  * B fragment addresses are lane-constant + immediate offsets (the slot swizzle depends on
+//    l32 only), A fragment addresses lane-constant + the buffer base;
+//  * interior tiles store without row / column guards; the channel-bias rows of a lane's 32
+//    rows are a bit mask computed once per tile.
+// ABL (ablation, tools only): 0 full; 1 no DMA / barriers (LDS contents stale); 2 also no
+// split (fragments reinterpreted); 3 also no LDS reads (MFMAs on register operands only).
+// NW waves (BM = 32 NW).  ST = 3: the ring above (one workgroup per CU at NW = 8).  ST = 2:
+// two buffers, the k-tile's own split at its top and one barrier per k-tile; at NW = 4,
+// TN = 8 a workgroup takes 64 KiB of LDS, so two share a CU and one's epilogue stores
+// overlap the other's MFMAs.
+template <int TN, int ABL = 0, int NW = 8, int ST = 3>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW))) void gemm_x6d_kernel(const float* __restrict__ X, int ldx,
+                                                       const uint16_t* __restrict__ Wp, int ldp,
+                                                       const float* __restrict__ bias, const float* R, int ldr,
+                                                       float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
+                                                       int ntn) {
+  constexpr int BM = 32 * NW, BN = 32 * TN, BK = 16;
+  constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NW - 1) / NW;
+  static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
+  static_assert(ST == 2 || ST == 3, "ring depth");
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+
+  const int nblk = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+
+  // per-lane DMA source offsets (bytes) relative to the scalar bases xa / wb, and LDS targets
+  uint32_t voff[PER], ldst[PER];
+  bool isA[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    int j = wid + t * NW;
+    if (j >= IA + IB) j = IA + IB - 1;  // wave-uniform: repeat the last piece
+    isA[t] = j < IA;
+    if (j < IA) {  // 16 rows x 64 B of f32 activations
+      const int r = j * 16 + (lane >> 2);
+      const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
+      voff[t] = (uint32_t)((size_t)r * ldx + sl) * 4u;
+      ldst[t] = j * 1024;
+    } else {  // 32 rows x 32 B of the weight planes, rows (plane, n) contiguous in LDS
+      const int q = (j - IA) * 32 + (lane >> 1);
+      const int p = q / BN, n = q % BN;
+      const int sl = ((lane & 1) ^ ((n >> 3) & 1)) * 8;
+      voff[t] = (uint32_t)(((size_t)p * ldp + n) * K + sl) * 2u;
+      ldst[t] = A_BYTES + (j - IA) * 1024;
+    }
+  }
+  const char* xa = reinterpret_cast<const char*>(X + (size_t)row0 * ldx);
+  const char* wb = reinterpret_cast<const char*>(Wp + (size_t)col0 * K);
+  auto stage = [&](int kt, int buf) {
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const char* base = isA[t] ? xa + kt * (BK * 4) : wb + kt * (BK * 2);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * STAGE) + ldst[t]);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(voff[t]), "s"(base), "s"(dst)
+                   : "memory");
+    }
+  };
+  // A fragment: row m, k = 8 lh + (0..7) = logical 16-B slots 2lh, 2lh+1 of a 64-B row
+  const int m = wid * 32 + l32;
+  const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
+  const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
+  // B fragment of column block j: row n = 32j + l32, slot lh ^ ((n >> 3) & 1) = lh ^ ((l32 >> 3) & 1)
+  const int boff = A_BYTES + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  const int nk = K / BK;
+  if (ST == 2) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* Bs = smem + boff;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(kt + 1, cur ^ 1);  // buffer last read in iteration kt-1
+      const char* As = smem + cur * STAGE;
+      bf16x8 c0, c1, c2;
+      {
+        const float4 u = *reinterpret_cast<const float4*>(As + aoff0);
+        const float4 v = *reinterpret_cast<const float4*>(As + aoff1);
+        split3(u, v, c0, c1, c2);
+      }
+      const char* Bc = Bs + cur * STAGE;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bc + j * 1024);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bc + B_PLANE + j * 1024);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bc + 2 * B_PLANE + j * 1024);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 landed
+      __syncthreads();                                  // ... and buffer cur is free
+    }
+  } else {
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bf16x8 c0, c1, c2;
+  {
+    const float4 u = *reinterpret_cast<const float4*>(smem + aoff0);
+    const float4 v = *reinterpret_cast<const float4*>(smem + aoff1);
+    split3(u, v, c0, c1, c2);
+  }
+  int bcur = 0;
+  bf16x8 rb0 = c0, rb1 = c1, rb2 = c2;  // ABL 3 operands
+  for (int kt = 0; kt < nk; ++kt) {
+    if (ABL == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued one iteration ago)
+      __syncthreads();
+    }
+    int bn1 = bcur + 1, bn2 = bcur + 2;
+    if (bn1 >= 3) bn1 -= 3;
+    if (bn2 >= 3) bn2 -= 3;
+    if (ABL == 0 && kt + 2 < nk) stage(kt + 2, bn2);
+    const bool more = kt + 1 < nk;
+    float4 u, v;
+    if (more) {
+      if (ABL < 3) {
+        const char* An = smem + bn1 * STAGE;  // ABL 3, 4: no LDS reads
+        u = *reinterpret_cast<const float4*>(An + aoff0);
+        v = *reinterpret_cast<const float4*>(An + aoff1);
+      } else {
+        u = make_float4(kt, 1.f, 2.f, 3.f);
+        v = u;
+      }
+    }
+    const char* Bs = smem + bcur * STAGE + boff;
+    bf16x8 n0, n1, n2;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 b0, b1, b2;
+      if (ABL < 3) {
+        b0 = *reinterpret_cast<const bf16x8*>(Bs + j * 1024);
+        b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + j * 1024);
+        b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + j * 1024);
+      } else {
+        b0 = rb0;
+        b1 = rb1;
+        b2 = rb2;
+      }
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
+      if (j == TN / 2 && more) {
+        if (ABL < 2) {
+          split3(u, v, n0, n1, n2);
+        } else {
+          n0 = __builtin_bit_cast(bf16x8, u);
+          n1 = __builtin_bit_cast(bf16x8, v);
+          n2 = n0;
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      c0 = n0;
+      c1 = n1;
+      c2 = n2;
+    }
+    bcur = bn1;
+  }
+  }  // ST == 3
+
+  if (ABL >= 4) {  // ablation: no stores unless the impossible happens (keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) t += acc[j][e];
+    if (t == 1234.5f) Y[tid] = t;
+    return;
+  }
+  // epilogue.  The MFMA operands are swapped (weight fragment as A), so register e of
+  // acc[j] holds output row rw0 + l32, column 32j + 8(e >> 2) + 4lh + (e & 3): four
+  // consecutive columns per register group.  Each wave transposes 32 x 64-column panels
+  // through a private LDS region (row stride 68 floats: conflict-free ds_write_b128) and
+  // writes whole 256-B row pieces with global_store_dwordx4 (4 rows per instruction; the
+  // residual is read the same way).  dword stores of the MFMA layout were store-issue bound.
+  __syncthreads();  // every wave is done with the ring buffers
+  const int rw0 = row0 + wid * 32;
+  float* red = reinterpret_cast<float*>(smem) + wid * (32 * 68);
+  const bool full = rw0 + 32 <= rows && col0 + BN <= ncols;
+  const int lr = lane >> 4, lc = (lane & 15) * 4;  // read-back: rows 4q + lr, columns lc..lc+3
+  uint32_t vq = 0;  // bit q: row rw0 + lr + 4q carries the bias (channel 0)
+  if (bias) {
+    if (C == 1) {
+      vq = 0xffu;
+    } else {
+      int t = (rw0 + lr) % C;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (t == 0) vq |= 1u << q;
+        t += 4;
+        while (t >= C) t -= C;
+      }
+    }
+  }
+#pragma unroll
+  for (int pnl = 0; pnl < TN / 2; ++pnl) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x16& a = acc[2 * pnl + jj];
+        *reinterpret_cast<float4*>(red + l32 * 68 + 32 * jj + 8 * g + 4 * lh) =
+            make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+      }
+    const int c = col0 + 64 * pnl + lc;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias && (full || c + 3 < ncols)) bv = *reinterpret_cast<const float4*>(bias + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int rr = 4 * q + lr, r = rw0 + rr;
+      float4 v = *reinterpret_cast<const float4*>(red + rr * 68 + lc);
+      if (full || (r < rows && c + 3 < ncols)) {
+        if (vq & (1u << q)) {
+          v.x += bv.x;
+          v.y += bv.y;
+          v.z += bv.z;
+          v.w += bv.w;
+        }
+        if (R) {
+          const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+          v.x += rv.x;
+          v.y += rv.y;
+          v.z += rv.z;
+          v.w += rv.w;
+        }
+        *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = v;
+      } else if (r < rows) {  // ragged edge: element by element
+        const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (c + t >= ncols) break;
+          float val = e4[t];
+          if (vq & (1u << q)) val += bias[c + t];
+          if (R) val += R[(size_t)r * ldr + c + t];
+          Y[(size_t)r * ldy + c + t] = val;
+        }
+      }
+    }
+  }
+}
+
+template <int TN, int ABL = 0, int NW = 8, int ST = 3>
+void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  constexpr int BM = 32 * NW, BN = 32 * TN;
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  // LDS: the DMA ring, reused by the epilogue's per-wave 32 x 68-float transpose regions
+  const size_t smem = std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)NW * 32 * 68 * 4);
+  ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST>, smem);
+  hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp, ldp,
+                     bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+}
+
+// ---- persistent lean form: one DMA ring across all of a workgroup's tiles --------------------
+// gemm_x6d_kernel (ST = 3) run persistently: the workgroup walks tiles blockIdx.x, +G, ...
+// and the (tile, k-tile) steps form one stream, so the next tile's first k-tiles are in
+// flight (and its first split done) while the current tile's epilogue runs; the epilogue
+// transposes through its own LDS region (not the ring) and its 4*TN dwordx4 stores stay
+// in flight under the next steps (counted: vmcnt(4*TN) at the next step's wait; VMEM ops of
+// a wave complete in order).  LDS: ring 3 x 40 KiB + 8 x 4.5 KiB transpose = 156 KiB.
+template <int TN, bool HAS_R>
+__global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__ X, int ldx,
+                                                       const uint16_t* __restrict__ Wp, int ldp,
+                                                       const float* __restrict__ bias, const float* R, int ldr,
+                                                       float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
+                                                       int ntn) {
+  constexpr int NW = 8, BM = 256, BN = 32 * TN, BK = 16;
+  constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
+  constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NW - 1) / NW;
+  constexpr int NST = 4 * TN, TS = 36;  // stores per wave per tile; transpose row stride (floats)
+  static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
+  static_assert(PER + NST <= 63, "vmcnt range");
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int nblk = ntm * ntn, G = gridDim.x;
+  const int my_tiles = ((int)blockIdx.x < nblk) ? (nblk - 1 - (int)blockIdx.x) / G + 1 : 0;
+  const int nk = K / BK, F = my_tiles * nk;
+  if (F == 0) return;
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto tile_of = [&](int i, int& row0, int& col0) {  // XCD-aware order (G is a multiple of 8)
+    const int idx = blockIdx.x + i * G;
+    const int q = nblk / 8, r8 = nblk % 8, xcd = idx % 8, slot = idx / 8;
+    const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+    row0 = (bid / ntn) * BM;
+    col0 = (bid % ntn) * BN;
+  };
+
+  uint32_t voff[PER], ldst[PER];
+  bool isA[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    int j = wid + t * NW;
+    if (j >= IA + IB) j = IA + IB - 1;
+    isA[t] = j < IA;
+    if (j < IA) {
+      const int r = j * 16 + (lane >> 2);
+      const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
+      voff[t] = (uint32_t)((size_t)r * ldx + sl) * 4u;
+      ldst[t] = j * 1024;
+    } else {
+      const int q = (j - IA) * 32 + (lane >> 1);
+      const int p = q / BN, n = q % BN;
+      const int sl = ((lane & 1) ^ ((n >> 3) & 1)) * 8;
+      voff[t] = (uint32_t)(((size_t)p * ldp + n) * K + sl) * 2u;
+      ldst[t] = A_BYTES + (j - IA) * 1024;
+    }
+  }
+  auto stage = [&](int f, int buf) {
+    int row0, col0;
+    tile_of(f / nk, row0, col0);
+    const int kt = f % nk;
+    const char* xa = reinterpret_cast<const char*>(X + (size_t)row0 * ldx) + kt * (BK * 4);
+    const char* wb = reinterpret_cast<const char*>(Wp + (size_t)col0 * K) + kt * (BK * 2);
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const char* base = isA[t] ? xa : wb;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * STAGE) + ldst[t]);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(voff[t]), "s"(base), "s"(dst)
+                   : "memory");
+    }
+  };
+  const int m = wid * 32 + l32;
+  const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
+  const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
+  const int boff = A_BYTES + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
+  float* red = reinterpret_cast<float*>(smem + 3 * STAGE) + wid * (32 * TS);
+  const int lr = lane >> 3, lc = (lane & 7) * 4;  // read-back: rows 8q + lr, columns lc..lc+3
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  stage(0, 0);
+  if (F > 1) stage(1, 1);
+  if (F > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bf16x8 c0, c1, c2;
+  {
+    const float4 u = *reinterpret_cast<const float4*>(smem + aoff0);
+    const float4 v = *reinterpret_cast<const float4*>(smem + aoff1);
+    split3(u, v, c0, c1, c2);
+  }
+  int bcur = 0, kt = 0, tile = 0;
+  bool stored = false;  // epilogue stores issued in the previous step
+  for (int f = 0; f < F; ++f) {
+    // wait for step f+1's DMA (issued one step ago); younger: the previous epilogue's stores
+    if (stored)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    stored = false;
+    int bn1 = bcur + 1, bn2 = bcur + 2;
+    if (bn1 >= 3) bn1 -= 3;
+    if (bn2 >= 3) bn2 -= 3;
+    if (f + 2 < F) stage(f + 2, bn2);
+    const bool more = f + 1 < F;
+    float4 u, v;
+    if (more) {
+      const char* An = smem + bn1 * STAGE;
+      u = *reinterpret_cast<const float4*>(An + aoff0);
+      v = *reinterpret_cast<const float4*>(An + aoff1);
+    }
+    const char* Bs = smem + bcur * STAGE + boff;
+    bf16x8 n0, n1, n2;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bs + j * 1024);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + j * 1024);
+      const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + j * 1024);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
+      if (j == TN / 2 && more) split3(u, v, n0, n1, n2);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      c0 = n0;
+      c1 = n1;
+      c2 = n2;
+    }
+    bcur = bn1;
+    if (++kt < nk) continue;
+    // ---- tile done: epilogue (MFMA layout: acc[j] reg e = row rw0 + l32, column
+    // 32j + 8(e>>2) + 4lh + (e&3)); transpose 32 x 32 blocks through `red`, dwordx4 stores
+    int row0, col0;
+    tile_of(tile, row0, col0);
+    kt = 0;
+    ++tile;
+    const int rw0 = row0 + wid * 32;
+    const bool full = rw0 + 32 <= rows && col0 + BN <= ncols;
+    uint32_t vq = 0;  // bit q: row rw0 + lr + 8q carries the bias
+    if (bias) {
+      if (C == 1) {
+        vq = 0xfu;
+      } else {
+        int t = (rw0 + lr) % C;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (t == 0) vq |= 1u << q;
+          t += 8;
+          while (t >= C) t -= C;
+        }
+      }
+    }
+    // Loads first: every load issued after a store would make its wait drain that store
+    // (vmcnt counts loads and stores in one in-order queue).  Bias slices of all column
+    // blocks up front; the residual of block j+1 before the stores of block j.  Interior
+    // tiles run branch-free (bias required; HAS_R a template flag), so the compiler's waits
+    // stay counted; partial tiles take a guarded element-wise path.
+    if (full) {
+      float4 bvv[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)  // vq == 0 without a bias: the zeros are never added
+        bvv[j] = bias ? *reinterpret_cast<const float4*>(bias + col0 + 32 * j + lc) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 rcur[4], rnext[4];
+      auto load_r = [&](int j, float4(&dst)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dst[q] = *reinterpret_cast<const float4*>(R + (size_t)(rw0 + 8 * q + lr) * ldr + col0 + 32 * j + lc);
+      };
+      if (HAS_R) load_r(0, rcur);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (HAS_R && j + 1 < TN) load_r(j + 1, rnext);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(red + l32 * TS + 8 * g + 4 * lh) =
+              make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = 8 * q + lr;
+          float4 val = *reinterpret_cast<const float4*>(red + rr * TS + lc);
+          if (vq & (1u << q)) {
+            val.x += bvv[j].x;
+            val.y += bvv[j].y;
+            val.z += bvv[j].z;
+            val.w += bvv[j].w;
+          }
+          if (HAS_R) {
+            val.x += rcur[q].x;
+            val.y += rcur[q].y;
+            val.z += rcur[q].z;
+            val.w += rcur[q].w;
+          }
+          *reinterpret_cast<float4*>(Y + (size_t)(rw0 + rr) * ldy + col0 + 32 * j + lc) = val;
+        }
+        if (HAS_R) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rcur[q] = rnext[q];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(red + l32 * TS + 8 * g + 4 * lh) =
+              make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+        const int c = col0 + 32 * j + lc;
+        for (int q = 0; q < 4; ++q) {
+          const int rr = 8 * q + lr, r = rw0 + rr;
+          if (r >= rows) continue;
+          const float* x4 = red + rr * TS + lc;
+          for (int t2 = 0; t2 < 4 && c + t2 < ncols; ++t2) {
+            float x = x4[t2];
+            if (vq & (1u << q)) x += bias[c + t2];
+            if (HAS_R) x += R[(size_t)r * ldr + c + t2];
+            Y[(size_t)r * ldy + c + t2] = x;
+          }
+        }
+      }
+    }
+    // full tiles issue exactly NST stores per wave (the count the next wait assumes);
+    // partial tiles drain everything at the next wait
+    stored = full;
+  }
+}
+
+template <int TN>
+void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  constexpr int BM = 256, BN = 32 * TN;
+  const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
+  const size_t smem = 3ull * (BM * 16 * 4 + 3 * BN * 16 * 2) + 8ull * 32 * 36 * 4;
+  int grid = std::min(ntm * ntn, cu_count_x6());
+  grid = std::max(8, grid / 8 * 8);
+  if (R) {
+    ensure_smem(gemm_x6q_kernel<TN, true>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, true>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
+                       ldy, rows, ncols, K, C, ntm, ntn);
+  } else {
+    ensure_smem(gemm_x6q_kernel<TN, false>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, false>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
+                       ldy, rows, ncols, K, C, ntm, ntn);
+  }
+}
+
+// ---- persistent form: weight panel resident in LDS, activations straight to registers ----
+// A workgroup owns one 64-column panel of the output for its whole life: the three bf16
+// planes of that weight panel (64 x K x 3 x 2 B = 96 KiB at K = 256) are loaded into LDS
+// once, then every wave walks its own 32-row tiles with NO barrier: it loads its A rows
+// from global memory straight into registers (lane (r, h) holds row r, k = 32t + 16h ..
+// +15 of k-tile t: 64 contiguous bytes, the two lane halves covering a 128-B line), one
+// k-tile ahead, splits them and runs 2 x 6 MFMAs per 16-k chunk against B fragments read
+// from LDS.  B k labelling matches: chunk c of k-tile t takes k = 32t + 16h + 8c + j.
+// LDS image: [plane][64 rows][K] bf16, 16-B slot s of row n stored at s ^ (n & 15).
+// Groups of P workgroups (one per panel, adjacent logical ids, i.e. one XCD) walk the
+// same row tiles, so each A row is fetched from HBM once and re-read from L2.
+constexpr int XP_BN = 64;
+
+template <int NW, bool HAS_R>
+__global__ __launch_bounds__(NW * 64) void gemm_x6p_kernel(const float* __restrict__ X, int ldx,
+                                                           const uint16_t* __restrict__ Wp, int ldp,
+                                                           const float* __restrict__ bias, const float* R, int ldr,
+                                                           float* Y, int ldy, int rows, int ncols, int K, int C,
+                                                           int P, int ngroups) {
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  // logical id: consecutive ids share an XCD (gridDim.x is a multiple of 8)
+  const int g = blockIdx.x, per_xcd = gridDim.x / 8;
+  const int L = (g % 8) * per_xcd + g / 8;
+  const int group = L / P, panel = L % P;
+  if (group >= ngroups) return;  // whole workgroup exits (no barrier reached)
+  const int col0 = panel * XP_BN;
+  const int row_bytes = K * 2, slots = K / 8;  // one B row: K bf16 = K/8 slots of 16 B
+  const int plane_bytes = XP_BN * row_bytes;
+  // ---- load the weight panel (three planes) into LDS, swizzled
+  {
+    const int total = 3 * XP_BN * slots;  // 16-B pieces
+    for (int q = tid; q < total; q += NW * 64) {
+      const int p = q / (XP_BN * slots), rem = q % (XP_BN * slots);
+      const int n = rem / slots, s = rem % slots;
+      const uint4 v =
+          *reinterpret_cast<const uint4*>(Wp + ((size_t)p * ldp + col0 + n) * K + (size_t)s * 8);
+      *reinterpret_cast<uint4*>(smem + p * plane_bytes + n * row_bytes + ((s ^ (n & 15)) * 16)) = v;
+    }
+  }
+  __syncthreads();
+
+  const int ntiles = (rows + 31) / 32, nk = K / 32;
+  // this wave's tiles: group + ngroups * (wid + NW * i)
+  const int first = group + ngroups * wid, stride = ngroups * NW;
+  const int my_tiles = first < ntiles ? (ntiles - 1 - first) / stride + 1 : 0;
+  const int F = my_tiles * nk;
+  if (F == 0) return;
+
+  auto load_a = [&](int f, float4 (&a)[4]) {
+    const int t = first + (f / nk) * stride, kt = f % nk;
+    const float* src = X + (size_t)(t * 32 + l32) * ldx + kt * 32 + lh * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  float4 an[4], ac[4];
+  load_a(0, an);
+  int kt = 0, tcount = 0;
+  for (int f = 0; f < F; ++f) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ac[q] = an[q];
+    if (f + 1 < F) load_a(f + 1, an);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf16x8 a0, a1, a2;
+      split3(ac[2 * c], ac[2 * c + 1], a0, a1, a2);
+      const int s = 4 * kt + 2 * lh + c;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = j * 32 + l32;
+        const char* bp = smem + n * row_bytes + ((s ^ (n & 15)) * 16);
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bp);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bp + plane_bytes);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(bp + 2 * plane_bytes);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[j], 0, 0, 0);
+      }
+    }
+    if (++kt == nk) {  // tile done: epilogue
+      const int t = first + tcount * stride;
+      const int rbase = t * 32 + 4 * lh;
+      const int rm0 = (C == 1) ? 0 : rbase % C;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = col0 + j * 32 + l32;
+        const bool cok = c < ncols;
+        const float bv = (bias && cok) ? bias[c] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int off = (e & 3) + 8 * (e >> 2);
+          const int r = rbase + off;
+          float v = acc[j][e];
+          acc[j][e] = 0.f;
+          if (!cok || r >= rows) continue;
+          if (bias) {
+            int tt = rm0 + off;
+            while (tt >= C) tt -= C;
+            if (tt == 0) v += bv;
+          }
+          if (HAS_R) v += R[(size_t)r * ldr + c];
+          Y[(size_t)r * ldy + c] = v;
+        }
+      }
+      kt = 0;
+      ++tcount;
+    }
+  }
+}
+
+template <int NW>
+void launch_x6p_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  const int P = (ncols + XP_BN - 1) / XP_BN;
+  const int slots = std::max(8, cu_count_x6() / 8 * 8);  // workgroups resident at once (1 per CU)
+  int ngroups = std::max(1, slots / P);
+  const int ntiles = (rows + 31) / 32;
+  ngroups = std::min(ngroups, std::max(1, (ntiles + NW - 1) / NW));
+  const int grid = round_up(ngroups * P, 8);
+  const size_t smem = 3ull * XP_BN * K * 2;
+  ensure_smem(gemm_x6p_kernel<NW, true>, smem);
+  ensure_smem(gemm_x6p_kernel<NW, false>, smem);
+  if (R)
+    hipLaunchKernelGGL((gemm_x6p_kernel<NW, true>), dim3(grid), dim3(NW * 64), smem, s, X, ldx, Wp, ldp, bias, R,
+                       ldr, Y, ldy, rows, ncols, K, C, P, ngroups);
+  else
+    hipLaunchKernelGGL((gemm_x6p_kernel<NW, false>), dim3(grid), dim3(NW * 64), smem, s, X, ldx, Wp, ldp, bias, R,
+                       ldr, Y, ldy, rows, ncols, K, C, P, ngroups);
+}
+
+// Wt[n][k] f32 (row stride ldw) -> three bf16 planes Wp[p][n][k], p = 0, 1, 2 (rows n >= ncols zero).
+__global__ void split_planes_kernel(const float* __restrict__ Wt, int ldw, int ncols, int K, int ldp, uint16_t* Wp) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t plane = (size_t)ldp * K;
+  if (i >= plane) return;
+  const int n = (int)(i / K), k = (int)(i % K);
+  const float a = n < ncols ? Wt[(size_t)n * ldw + k] : 0.f;
+  const __bf16 a0 = (__bf16)a;
+  const float r1 = a - (float)a0;
+  const __bf16 a1 = (__bf16)r1;
+  const __bf16 a2 = (__bf16)(r1 - (float)a1);
+  Wp[i] = __builtin_bit_cast(uint16_t, a0);
+  Wp[plane + i] = __builtin_bit_cast(uint16_t, a1);
+  Wp[2 * plane + i] = __builtin_bit_cast(uint16_t, a2);
+}
+
+}  // namespace
+
+int x6_plane_rows(int ncols) { return round_up(ncols, kRowPad) + kRowPad; }
+
+void launch_split_planes(const float* Wt, int ldw, int ncols, int K, uint16_t* Wp, hipStream_t s) {
+  const int ldp = x6_plane_rows(ncols);
+  const size_t n = (size_t)ldp * K;
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Wt, ldw, ncols, K, ldp,
+                     Wp);
+}
+
+bool gemm_x6_supported(int K) { return K % X6_BK == 0; }
+
+void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
+                            hipStream_t s) {
+  switch (v) {
+    case 1:
+      launch_x6_t<4, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 2:
+      launch_x6_t<4, 8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 3:
+      launch_x6_t<8, 6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 4:
+      launch_x6_t<4, 6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 5:
+      launch_x6_t<2, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 6:
+      launch_x6_t<2, 8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 7:
+      launch_x6_t<8, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // persistent, weight panel resident in LDS (K <= 256)
+    case 10:
+      launch_x6p_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 11:
+      launch_x6p_t<12>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 12:
+      launch_x6p_t<16>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 13:
+      launch_x6p_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // big tiles 256 x 64*TN, BK = 16
+    case 20:
+      launch_x6b_t<4, 3>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 21:
+      launch_x6b_t<4, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 22:
+      launch_x6b_t<3, 3>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 23:
+      launch_x6b_t<2, 3>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // pipelined 256 x 32*TN
+    case 30:
+      launch_x6c_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 31:
+      launch_x6c_t<6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 32:
+      launch_x6c_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // lean pipelined 256 x 32*TN
+    case 40:
+      launch_x6d_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 41:
+      launch_x6d_t<6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 42:
+      launch_x6d_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // two workgroups per CU: 128 x 32*TN tiles, two buffers
+    case 43:
+      launch_x6d_t<8, 0, 4, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 44:
+      launch_x6d_t<6, 0, 4, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 45:
+      launch_x6d_t<4, 0, 4, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 46:
+      launch_x6d_t<4, 0, 8, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // persistent lean
+    case 50:
+      launch_x6q_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 51:
+      launch_x6q_t<6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 52:
+      launch_x6q_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // ablations of variant 40 (wrong results; tools/gemm_bench.py only)
+    case 91:
+      launch_x6d_t<8, 1>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 92:
+      launch_x6d_t<8, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 93:
+      launch_x6d_t<8, 3>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 94:
+      launch_x6d_t<8, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    default:
+      launch_x6_t<8, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+  }
+}
+
+void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+  // measured on MI355X (tools/gemm_bench.py, K = 256): channel rows take the persistent lean
+  // kernel with 256 x 256 tiles (256 x 192 when ncols is a multiple of 192 only); short
+  // (log-psi) row counts take 256 x 128 tiles, two workgroups per CU.
+  int v;
+  if (rows >= 65536)
+    v = (ncols % 192 == 0 && ncols % 256 != 0) ? 51 : 50;
+  else
+    v = (ncols % 192 == 0 && ncols % 256 != 0) ? 44 : 46;
+  launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+}
+
+}  // namespace dh

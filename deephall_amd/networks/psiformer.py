@@ -19,6 +19,7 @@ per-device handle and workspace.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 from dataclasses import dataclass
 
@@ -95,6 +96,11 @@ class NativeHandle:
         self.nparams = self.offsets[-1]
         self.ws = {}  # one workspace per HIP stream (walker groups may run on parallel streams)
         self._params_key = None
+        self.set_gemm_mode(_GEMM_MODE)
+
+    def set_gemm_mode(self, mode: str):
+        """Local-energy GEMM arithmetic: "x6" (split-bf16, f32-accurate; default) or "f32"."""
+        _lib.check(self.lib.dh_set_gemm_mode(self.h, _GEMM_MODES[mode]))
 
     def __del__(self):
         try:
@@ -121,6 +127,22 @@ class NativeHandle:
         _lib.check(self.lib.dh_set_params(self.h, _ptr(packed), self.nparams, _stream(self.device)))
         self._packed = packed  # keep alive while the copy is in flight
         self._params_key = key
+
+
+_GEMM_MODES = {"f32": 0, "x6": 1}
+_GEMM_MODE = os.environ.get("DH_GEMM", "x6")
+if _GEMM_MODE not in _GEMM_MODES:
+    raise ValueError(f"DH_GEMM must be one of {sorted(_GEMM_MODES)}, got {_GEMM_MODE!r}")
+
+
+def set_gemm_mode(mode: str):
+    """Select the local-energy GEMM arithmetic for every handle (existing and future)."""
+    global _GEMM_MODE
+    if mode not in _GEMM_MODES:
+        raise ValueError(f"GEMM mode must be one of {sorted(_GEMM_MODES)}")
+    _GEMM_MODE = mode
+    for h in _HANDLES.values():
+        h.set_gemm_mode(mode)
 
 
 def get_handle(spec: NetworkSpec, device) -> NativeHandle:

@@ -103,6 +103,17 @@ int dh_param_layout(const dh_handle* h, size_t* offsets, int n);
  * handle.  `count` must equal the total from dh_param_layout. */
 int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream);
 
+/* GEMM arithmetic of the local-energy (2N+5 channel) pass:
+ *   DH_GEMM_F32   exact-f32 MFMA (v_mfma_f32_32x32x2_f32), f32 rounding per product;
+ *   DH_GEMM_X6    split-bf16 MFMA: each f32 operand split exactly into three bf16 terms,
+ *                 six bf16 products per pair (dropped terms <= 2^-24 |ab|, f32 accumulate);
+ *                 error at the level of the f32 GEMM (tests/test_gpu_kernels.py), 2.67x the
+ *                 f32 matrix rate.  Default.
+ * The log-psi / MCMC passes always use the exact-f32 kernels. */
+#define DH_GEMM_F32 0
+#define DH_GEMM_X6 1
+int dh_set_gemm_mode(dh_handle* h, int mode);
+
 /* Workspace bytes needed to process `batch` walkers: op 0 = log psi / MCMC,
  * op 1 = local energy.  Local energy processes walkers in chunks sized to the
  * workspace it is given (at least one walker). */
@@ -186,6 +197,15 @@ int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw,
  * bm = rows per workgroup (32, 64, 96; 0 = automatic).  X, h hold round_up(rows, 96) rows. */
 int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
                      const float* ln, float* h, int rows, int K, void* stream);
+
+/* Test hooks of the split-bf16 GEMM (gemm_x6.hip): the transposed weight Wt[ncols][K]
+ * is split into three bf16 planes Wp[3][ldp][K] (ldp = dh_debug_x6_plane_rows(ncols),
+ * uint16 bit patterns), then Y = X Wt^T (+ bias on rows r % C == 0) (+ R) with
+ * K % 32 == 0 and X holding round_up(rows, 256) rows; variant -1 = automatic. */
+int dh_debug_x6_plane_rows(int ncols);
+int dh_debug_split_planes(const float* Wt, int ldw, int ncols, int K, uint16_t* Wp, void* stream);
+int dh_debug_gemm_x6(int variant, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                     const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C, void* stream);
 
 /* init_guess with the device RNG: theta = arccos U(-1,1), phi = U(-pi,pi). */
 int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream);

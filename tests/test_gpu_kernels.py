@@ -73,6 +73,66 @@ def test_gemm_variants(cuda, variant):
             assert torch.isnan(Y[rows:]).all()  # rows past `rows` untouched
 
 
+X6_VARIANTS = [-1, 0, 12, 40, 41, 43, 44, 45, 46, 50, 51, 52]
+
+
+def _x6_planes(lib, W, n, K):
+    ldp = lib.dh_debug_x6_plane_rows(n)
+    Wt = W.t().contiguous()
+    Wp = torch.empty(3 * ldp * K, dtype=torch.int16, device="cuda")
+    assert lib.dh_debug_split_planes(_p(Wt), K, n, K, _p(Wp), _stream()) == 0
+    return Wp, ldp
+
+
+def test_x6_split_planes_exact(cuda):
+    """The three bf16 planes sum exactly to the f32 weight (and zero-pad rows >= ncols)."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    K, n = 256, 192
+    W = (torch.randn(K, n, generator=g) * torch.exp(4 * torch.randn(K, n, generator=g))).cuda()
+    Wp, ldp = _x6_planes(lib, W, n, K)
+    torch.cuda.synchronize()
+    planes = Wp.view(3, ldp, K)
+    # bf16 bit pattern -> f32: shift into the high half
+    f = (planes.to(torch.int32) << 16).view(torch.float32).double()
+    recon = f[0] + f[1] + f[2]
+    assert torch.equal(recon[:n], W.t().double())
+    assert (recon[n:] == 0).all()
+    # the terms shrink by 2^-8 each (round to nearest)
+    assert (f[1].abs() <= f[0].abs() * 2.0**-8).all() and (f[2].abs() <= f[1].abs() * 2.0**-8).all()
+
+
+@pytest.mark.parametrize("variant", X6_VARIANTS)
+def test_gemm_x6_variants(cuda, variant):
+    """Split-bf16 GEMM: correct contract (bias rule, residual, ragged rows / columns) and an
+    error vs float64 at the level of the exact-f32 MFMA kernel on the same data."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(100 + variant)
+    for rows, n, K, Cc in SHAPES + [(4096, 480, 256, 1), (2048, 256, 256, 17)]:
+        rp = (rows + 255) // 256 * 256
+        X = torch.randn(rp, K, generator=g).cuda()
+        W = (torch.randn(K, n, generator=g) / 16).cuda()
+        b = torch.randn(n, generator=g).cuda() if rows != 2048 else None  # one case without a bias
+        R = torch.randn(rp, n, generator=g).cuda() if n == 256 else None
+        Wp, ldp = _x6_planes(lib, W, n, K)
+        Yb = torch.full((rp, n), float("nan"), device="cuda")
+        rc = lib.dh_debug_gemm_x6(variant, _p(X), K, _p(Wp), ldp, _p(b), _p(R), n, _p(Yb), n, rows, n, K, Cc,
+                                  _stream())
+        assert rc == 0
+        # exact-f32 MFMA kernel on the same data
+        Wt = torch.zeros((n + 255) // 256 * 256, K, device="cuda")
+        Wt[:n] = W.t()
+        Yf = torch.full((rp, n), float("nan"), device="cuda")
+        assert lib.dh_debug_gemm(106, _p(X), K, _p(Wt), K, _p(b), _p(R), n, _p(Yf), n, rows, n, K, Cc, _stream()) == 0
+        torch.cuda.synchronize()
+        ref, scale = _ref(X, W, b, R, rows, Cc)
+        err = ((Yb[:rows].double() - ref).abs() / scale).max().item()
+        err_f32 = ((Yf[:rows].double() - ref).abs() / scale).max().item()
+        assert err < 2e-5, (variant, rows, n, err)
+        assert err <= 2.0 * err_f32 + 1e-8, (variant, rows, n, err, err_f32)
+        assert torch.isnan(Yb[rows:]).all()
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("bm", [0, 32, 64, 96])
 @pytest.mark.parametrize("rows", [96, 1000, 24576])

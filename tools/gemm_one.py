@@ -1,4 +1,7 @@
-"""Run one GEMM variant on one C2 hot-path shape a few times (for rocprofv3 --pmc)."""
+"""Run one GEMM variant on one C2 hot-path shape a few times (for rocprofv3 --pmc).
+
+variant < 200: dh_debug_gemm (>= 100: NT kernels); variant >= 200: split-bf16 kernel
+variant - 200 through dh_debug_gemm_x6 (199 = automatic choice)."""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -17,8 +20,17 @@ W = torch.randn(K, n, device="cuda") / 16
 Wt = torch.zeros((n + 255) // 256 * 256, K, device="cuda")
 Wt[:n] = W.t()
 Y = torch.empty(rp, n, device="cuda")
+b = torch.randn(n, device="cuda")  # a bias, as on the hot path
 s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-Wa, ldw = (Wt, K) if v >= 100 else (W, n)
-for _ in range(reps):
-    assert lib.dh_debug_gemm(v, p(X), K, p(Wa), ldw, C.c_void_p(0), C.c_void_p(0), 0, p(Y), n, rows, n, K, 1, s) == 0
+null = C.c_void_p(0)
+if v >= 199:
+    ldp = lib.dh_debug_x6_plane_rows(n)
+    Wp = torch.empty(3 * ldp * K, dtype=torch.int16, device="cuda")
+    assert lib.dh_debug_split_planes(p(Wt), K, n, K, p(Wp), s) == 0
+    for _ in range(reps):
+        assert lib.dh_debug_gemm_x6(v - 200, p(X), K, p(Wp), ldp, p(b), null, 0, p(Y), n, rows, n, K, 1, s) == 0
+else:
+    Wa, ldw = (Wt, K) if v >= 100 else (W, n)
+    for _ in range(reps):
+        assert lib.dh_debug_gemm(v, p(X), K, p(Wa), ldw, p(b), null, 0, p(Y), n, rows, n, K, 1, s) == 0
 torch.cuda.synchronize()
