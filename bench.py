@@ -30,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "local-energies/sec + MCMC walker-steps/sec, N=6 2Q=15, 1/2/4/8 GPUs"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_F32_MFMA_TFLOPS  # same guide: f32 MFMA = 1/16 of BF16 (~2.5 PF dense)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -174,33 +175,55 @@ def main():
                 "ms_per_step": ms / args.steps,
                 "avg_us": 1e3 * ms / cnt,
             }
-    # HBM traffic per GEMM launch: rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes)
-    # of this same workload, committed by tools/profile_round.sh; only for the default config
+    from deephall_amd.networks import psiformer as _pf
+
+    gemm_mode = _pf._GEMM_MODE
+    x6 = gemm_mode in ("x6", "x6all")
+    # HBM traffic per channel-GEMM launch: rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate
+    # passes) of this same workload, committed by tools/profile_round.sh; default config only
     traffic = traffic_src = None
     tf = ROOT / "profiles" / "gemm_traffic.json"
     if tf.exists() and (B, tuple(args.nspins), args.flux, steps) == (4096, (6, 0), 15, 10):
         tj = json.loads(tf.read_text())
-        traffic = tj.get("gemm_bytes_per_launch")
-        traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})"
-    # dominant kernel: gemm_nt_kernel, all its launches in the instrumented region (log-psi
-    # and local-energy GEMMs; classes 0 and 7 of dh_profile_read)
-    ig = kinds.index("gemm_ch")
-    g_cnt, g_ms, g_fl, g_by = (prof[q] + prof[4 * ig + q] for q in range(4))
+        traffic = tj.get("channel_gemm_bytes_per_launch") if x6 else None
+        traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})" if traffic else None
+    # dominant kernel: the local-energy channel GEMM (class gemm_ch of dh_profile_read; in
+    # the split-bf16 modes the gemm_x6q_kernel family, ~29 % of the step).  Its arithmetic
+    # runs as 6 bf16 MFMA products per f32 product, so the ceiling of its algorithmic f32
+    # flop rate is the dense bf16 MFMA peak / 6.  The log-psi GEMMs (class gemm: exact-f32
+    # gemm_ln_kernel + split-bf16 gemm_x6d_kernel) are reported beside it.
+    def _cls(name):
+        i = kinds.index(name)
+        return prof[4 * i], prof[4 * i + 1], prof[4 * i + 2], prof[4 * i + 3]
+
+    g_cnt, g_ms, g_fl, g_by = _cls("gemm_ch")
+    l_cnt, l_ms, l_fl, l_by = _cls("gemm")
     achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
+    peak = PEAK_BF16_MFMA_TFLOPS / 6 if x6 else PEAK_F32_MFMA_TFLOPS
     roofline = {
-        "kernel": "gemm_nt_kernel (LDS-DMA staged, v_mfma_f32_32x32x2_f32)",
+        "kernel": ("gemm_x6q_kernel (local-energy channel GEMMs: persistent split-bf16 f32 GEMM, "
+                   "v_mfma_f32_32x32x16_bf16)" if x6 else "gemm_ntp_kernel (exact-f32 channel GEMMs)"),
         "bound": "mfma",
         "achieved": round(achieved, 2),
-        "peak": PEAK_F32_MFMA_TFLOPS,
+        "peak": round(peak, 1),
         "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+        "frac": round(achieved / peak, 4),
         "traffic": traffic,
+        "peak_basis": ("dense bf16 MFMA 2516.8 TF/s / 6 bf16 products per f32 product "
+                       "(algorithmic f32 flops)" if x6 else "dense f32 MFMA 157.3 TF/s"),
+        "achieved_over_f32_mfma_peak": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
         "flops_per_launch": g_fl / g_cnt if g_cnt else 0,
         "avg_launch_us": 1e3 * g_ms / g_cnt if g_cnt else 0,
-        "gemm_share_of_step": round(g_ms / (dt_prof * 1e3), 4) if g_ms else None,
+        "share_of_step": round(g_ms / (dt_prof * 1e3), 4) if g_ms else None,
         "measured_over": f"{args.steps} instrumented VMC steps (HIP event pair per launch)",
         "traffic_source": traffic_src,
         "bytes_per_launch_algorithmic": g_by / g_cnt if g_cnt else 0,
+        "logpsi_gemms": {
+            "launches_per_step": l_cnt / args.steps,
+            "avg_launch_us": 1e3 * l_ms / l_cnt if l_cnt else 0,
+            "achieved_tflops": round((l_fl / (l_ms * 1e-3)) / 1e12, 2) if l_ms > 0 else 0.0,
+            "share_of_step": round(l_ms / (dt_prof * 1e3), 4) if l_ms else None,
+        },
     } if not args.no_kernel_events else None
     B_total = B * world
     value = B_total * args.steps / dt
@@ -225,6 +248,7 @@ def main():
             "global_batch": B_total,
             "parallelism": f"walker-dp{world}",
             "walker_groups_per_gpu": args.groups,
+            "gemm_arithmetic": gemm_mode,
         },
         "walker_steps_per_sec": round(value * steps, 1),
         "components": {

@@ -98,7 +98,7 @@ struct dh_handle {
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
   float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
   uint16_t* wp = nullptr;  // split-bf16 weight planes for the x6 kernels (device)
-  int gemm_mode = DH_GEMM_X6;
+  int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
   bool params_set = false;
   Profiler prof;
@@ -308,7 +308,7 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
 
 int dh_set_gemm_mode(dh_handle* h, int mode) {
   if (!h) return fail(DH_EINVAL, "null handle");
-  if (mode != DH_GEMM_F32 && mode != DH_GEMM_X6) return fail(DH_EINVAL, "bad GEMM mode");
+  if (mode != DH_GEMM_F32 && mode != DH_GEMM_X6 && mode != DH_GEMM_X6_ALL) return fail(DH_EINVAL, "bad GEMM mode");
   h->gemm_mode = mode;
   return DH_OK;
 }
@@ -330,9 +330,15 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const int D = d.D;
   const double R = rows, DD = D, f4 = 4.0;
   const bool nt = P.WorbT != nullptr;
+  // channel rows (local energy) take the split-bf16 GEMM unless exact-f32 is requested;
+  // the log-psi rows only in DH_GEMM_X6_ALL.  The two log-psi GEMMs that carry a LayerNorm
+  // stay on the exact-f32 gemm_ln_kernel in every mode: at 24576 x 256 x 256 it takes
+  // 42 / 47 us against 42 / 53 us for the split-bf16 form with the same epilogue
+  // (launch_gemm_x6_ln) and 33 + 16 us for split-bf16 + a separate LayerNorm launch
+  // (tools/ln_gemm_bench.py on MI355X); the short GEMMs there are epilogue/latency bound.
+  const bool x6 = nt && gemm_x6_supported(D) &&
+                  (C > 1 ? h->gemm_mode != DH_GEMM_F32 : h->gemm_mode == DH_GEMM_X6_ALL);
   const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
-  // channel rows (local energy) take the split-bf16 GEMM unless exact-f32 is requested
-  const bool x6 = nt && C > 1 && h->gemm_mode == DH_GEMM_X6 && gemm_x6_supported(D);
   auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, const uint16_t* Wp, int ldw,
                   const float* bias, const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
     PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
@@ -532,6 +538,14 @@ int dh_debug_gemm_x6(int variant, const float* X, int ldx, const uint16_t* Wp, i
     launch_gemm_x6(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, (hipStream_t)stream);
   else
     launch_gemm_x6_variant(variant, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_debug_gemm_x6_ln(int mode, int nw, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                        const float* ln, float* h, int rows, int K, void* stream) {
+  if (!gemm_x6_supported(K) || K > 256 || ldp < x6_plane_rows(256) || rows < 1 || (mode != 0 && mode != 1))
+    return fail(DH_EINVAL, "bad gemm_x6_ln args");
+  launch_gemm_x6_ln(X, ldx, Wp, ldp, bias, ln, h, rows, K, mode, nw, (hipStream_t)stream);
   return check_launch();
 }
 

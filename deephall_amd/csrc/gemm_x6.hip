@@ -574,12 +574,21 @@ void launch_x6c_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
 // two buffers, the k-tile's own split at its top and one barrier per k-tile; at NW = 4,
 // TN = 8 a workgroup takes 64 KiB of LDS, so two share a CU and one's epilogue stores
 // overlap the other's MFMAs.
-template <int TN, int ABL = 0, int NW = 8, int ST = 3>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW))) void gemm_x6d_kernel(const float* __restrict__ X, int ldx,
+// LNM != 0 (log-psi rows, BN = ncols = 256, C = 1): the LayerNorm that follows the GEMM
+// runs in the epilogue, in place over h = R = Y (as gemm_ln_kernel, gemm.hip):
+//   LNM 1:  h = LN(h + X W + b)          (psiformer.py:44-45)
+//   LNM 2:  h = LN(h + tanh(X W + b))    (psiformer.py:46-47; X = h)
+// A workgroup owns whole rows, so the row statistics are wave-local: each wave transposes
+// its 32 x 256 block into LDS once, then sweeps it three times (pre-LN value + mean,
+// centred variance, normalise + store) with 16 lanes per row.  X (= h in LNM 2) is only
+// read by the DMA of this workgroup's own rows, all landed before the epilogue barrier.
+template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW))) void gemm_x6d_kernel(const float* X, int ldx,
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
                                                        float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
-                                                       int ntn) {
+                                                       int ntn, const float* __restrict__ ln) {
+  static_assert(LNM == 0 || TN == 8, "LayerNorm epilogue needs whole 256-column rows");
   constexpr int BM = 32 * NW, BN = 32 * TN, BK = 16;
   constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
   constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NW - 1) / NW;
@@ -778,6 +787,94 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
   // residual is read the same way).  dword stores of the MFMA layout were store-issue bound.
   __syncthreads();  // every wave is done with the ring buffers
   const int rw0 = row0 + wid * 32;
+  if constexpr (LNM != 0) {
+    constexpr int LS = 260;  // row stride (floats): conflict-free ds_write_b128, as 68 below
+    float* blk = reinterpret_cast<float*>(smem) + wid * (32 * LS);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(blk + l32 * LS + 32 * j + 8 * g + 4 * lh) =
+            make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
+    const int lr = lane >> 4, lc = (lane & 15) * 4;  // rows 4q + lr, columns 64p + lc .. +3
+    float mean[8], rstd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mean[q] = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int c = 64 * p + lc;
+      const float4 bv = *reinterpret_cast<const float4*>(bias + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 4 * q + lr, r = rw0 + rr;
+        float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
+        v.x += bv.x;
+        v.y += bv.y;
+        v.z += bv.z;
+        v.w += bv.w;
+        if (LNM == 2) {
+          v.x = tanhf(v.x);
+          v.y = tanhf(v.y);
+          v.z = tanhf(v.z);
+          v.w = tanhf(v.w);
+        }
+        if (r < rows) {
+          const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+          v.x += rv.x;
+          v.y += rv.y;
+          v.z += rv.z;
+          v.w += rv.w;
+        }
+        *reinterpret_cast<float4*>(blk + rr * LS + c) = v;
+        mean[q] += (v.x + v.y) + (v.z + v.w);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float t = mean[q];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64);
+      mean[q] = t * (1.f / 256.f);
+      rstd[q] = 0.f;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(blk + (4 * q + lr) * LS + 64 * p + lc);
+        const float dx = v.x - mean[q], dy = v.y - mean[q], dz = v.z - mean[q], dw = v.w - mean[q];
+        rstd[q] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float t = rstd[q];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64);
+      rstd[q] = 1.f / sqrtf(t * (1.f / 256.f) + 1e-5f);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int c = 64 * p + lc;
+      const float4 gm = *reinterpret_cast<const float4*>(ln + c);
+      const float4 bt = *reinterpret_cast<const float4*>(ln + 256 + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 4 * q + lr, r = rw0 + rr;
+        const float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
+        float4 o;
+        o.x = gm.x * (rstd[q] * (v.x - mean[q])) + bt.x;
+        o.y = gm.y * (rstd[q] * (v.y - mean[q])) + bt.y;
+        o.z = gm.z * (rstd[q] * (v.z - mean[q])) + bt.z;
+        o.w = gm.w * (rstd[q] * (v.w - mean[q])) + bt.w;
+        if (r < rows) *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = o;
+      }
+    }
+    return;
+  }
   float* red = reinterpret_cast<float*>(smem) + wid * (32 * 68);
   const bool full = rw0 + 32 <= rows && col0 + BN <= ncols;
   const int lr = lane >> 4, lc = (lane & 15) * 4;  // read-back: rows 4q + lr, columns lc..lc+3
@@ -842,16 +939,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
   }
 }
 
-template <int TN, int ABL = 0, int NW = 8, int ST = 3>
+template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0>
 void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
-                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, const float* ln = nullptr) {
   constexpr int BM = 32 * NW, BN = 32 * TN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
   // LDS: the DMA ring, reused by the epilogue's per-wave 32 x 68-float transpose regions
-  const size_t smem = std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)NW * 32 * 68 * 4);
-  ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST>, smem);
-  hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp, ldp,
-                     bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
+  // (32 x 260 floats, whole rows, with the LayerNorm epilogue)
+  const size_t smem =
+      std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)NW * 32 * (LNM ? 260 : 68) * 4);
+  ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST, LNM>, smem);
+  hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST, LNM>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp,
+                     ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln);
 }
 
 // ---- persistent lean form: one DMA ring across all of a workgroup's tiles --------------------
@@ -1415,6 +1514,28 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
   else
     v = (ncols % 192 == 0 && ncols % 256 != 0) ? 44 : 46;
   launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+}
+
+
+// log-psi GEMM + LayerNorm (LNM 1 / 2 above), in place over h [rows][256].  Tile height
+// 32 * nw rows (nw 3 or 4; 0 = choose): one workgroup per CU (LDS), so the height is picked
+// to fill the CUs with the fewest tile rounds; callers pad rows to 256 and a tile never
+// reads X past round_up(rows, 256).
+void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
+                       float* h, int rows, int K, int mode, int nw, hipStream_t s) {
+  if (nw != 3 && nw != 4) {
+    const int cu = cu_count_x6();
+    auto cost = [&](int w) { return ((rows + 32 * w - 1) / (32 * w) + cu - 1) / cu * w; };
+    nw = (cost(3) < cost(4) && round_up(rows, 96) <= round_up(rows, 256)) ? 3 : 4;
+  }
+#define DH_X6LN(NWV, M) \
+  launch_x6d_t<8, 0, NWV, 3, M>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln)
+  if (nw == 3) {
+    if (mode == 0) DH_X6LN(3, 1); else DH_X6LN(3, 2);
+  } else {
+    if (mode == 0) DH_X6LN(4, 1); else DH_X6LN(4, 2);
+  }
+#undef DH_X6LN
 }
 
 }  // namespace dh

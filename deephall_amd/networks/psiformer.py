@@ -99,7 +99,8 @@ class NativeHandle:
         self.set_gemm_mode(_GEMM_MODE)
 
     def set_gemm_mode(self, mode: str):
-        """Local-energy GEMM arithmetic: "x6" (split-bf16, f32-accurate; default) or "f32"."""
+        """GEMM arithmetic: "x6all" (split-bf16, f32-accurate, every GEMM; default), "x6"
+        (split-bf16 for the local-energy channel rows only) or "f32" (exact-f32 MFMA)."""
         _lib.check(self.lib.dh_set_gemm_mode(self.h, _GEMM_MODES[mode]))
 
     def __del__(self):
@@ -129,8 +130,8 @@ class NativeHandle:
         self._params_key = key
 
 
-_GEMM_MODES = {"f32": 0, "x6": 1}
-_GEMM_MODE = os.environ.get("DH_GEMM", "x6")
+_GEMM_MODES = {"f32": 0, "x6": 1, "x6all": 2}
+_GEMM_MODE = os.environ.get("DH_GEMM", "x6all")
 if _GEMM_MODE not in _GEMM_MODES:
     raise ValueError(f"DH_GEMM must be one of {sorted(_GEMM_MODES)}, got {_GEMM_MODE!r}")
 

@@ -108,10 +108,14 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
  *   DH_GEMM_X6    split-bf16 MFMA: each f32 operand split exactly into three bf16 terms,
  *                 six bf16 products per pair (dropped terms <= 2^-24 |ab|, f32 accumulate);
  *                 error at the level of the f32 GEMM (tests/test_gpu_kernels.py), 2.67x the
- *                 f32 matrix rate.  Default.
- * The log-psi / MCMC passes always use the exact-f32 kernels. */
+ *                 f32 matrix rate.
+ *   DH_GEMM_X6_ALL  split-bf16 also for the log-psi / MCMC GEMMs without a LayerNorm
+ *                 epilogue (q|k|v, orbitals); the LayerNorm-carrying ones stay exact-f32
+ *                 (measured faster at log-psi row counts).  Default.
+ * In DH_GEMM_F32 and DH_GEMM_X6 the log-psi / MCMC passes use the exact-f32 kernels. */
 #define DH_GEMM_F32 0
 #define DH_GEMM_X6 1
+#define DH_GEMM_X6_ALL 2
 int dh_set_gemm_mode(dh_handle* h, int mode);
 
 /* Workspace bytes needed to process `batch` walkers: op 0 = log psi / MCMC,
@@ -197,6 +201,11 @@ int dh_debug_gemm(int variant, const float* X, int ldx, const float* W, int ldw,
  * bm = rows per workgroup (32, 64, 96; 0 = automatic).  X, h hold round_up(rows, 96) rows. */
 int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
                      const float* ln, float* h, int rows, int K, void* stream);
+
+/* Split-bf16 form of dh_debug_gemm_ln (weight as the planes of dh_debug_split_planes,
+ * ldp >= dh_debug_x6_plane_rows(256)); nw = tile height / 32: 3, 4 or 0 (choose). */
+int dh_debug_gemm_x6_ln(int mode, int nw, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                        const float* ln, float* h, int rows, int K, void* stream);
 
 /* Test hooks of the split-bf16 GEMM (gemm_x6.hip): the transposed weight Wt[ncols][K]
  * is split into three bf16 planes Wp[3][ldp][K] (ldp = dh_debug_x6_plane_rows(ncols),

@@ -161,3 +161,35 @@ def test_gemm_layernorm_fused(cuda, mode, bm, rows):
     err = (h[:rows].double() - ref).abs().max().item()
     assert err < 2e-4, err
     assert torch.equal(h[rows:], h0[rows:])  # padding rows untouched
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("nw", [0, 3, 4])
+@pytest.mark.parametrize("rows", [96, 1000, 24576])
+def test_gemm_x6_layernorm_fused(cuda, mode, nw, rows):
+    """Split-bf16 log-psi GEMM with the LayerNorm in its epilogue (in place over h): same
+    contract and tolerance as the exact-f32 gemm_ln_kernel above, against float64."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(23 * mode + nw + rows)
+    K, D = 256, 256
+    rp = (rows + 767) // 768 * 768
+    X = torch.randn(rp, K, generator=g).cuda()
+    W = (torch.randn(K, D, generator=g) / 16).cuda()
+    Wp, ldp = _x6_planes(lib, W, D, K)
+    b = torch.randn(D, generator=g).cuda()
+    ln = torch.cat([1.0 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)]).cuda()
+    h0 = torch.randn(rp, D, generator=g).cuda()
+    if mode == 1:
+        X = h0
+    h = h0.clone()
+    Xin = h if mode == 1 else X
+    assert lib.dh_debug_gemm_x6_ln(mode, nw, _p(Xin), K, _p(Wp), ldp, _p(b), _p(ln), _p(h), rows, K, _stream()) == 0
+    torch.cuda.synchronize()
+    z = X[:rows].double() @ W.double() + b.double()
+    y = h0[:rows].double() + (z if mode == 0 else torch.tanh(z))
+    mu = y.mean(-1, keepdim=True)
+    var = ((y - mu) ** 2).mean(-1, keepdim=True)
+    ref = (y - mu) / torch.sqrt(var + 1e-5) * ln[:D].double() + ln[D:].double()
+    err = (h[:rows].double() - ref).abs().max().item()
+    assert err < 2e-4, err
+    assert torch.equal(h[rows:], h0[rows:])
