@@ -331,11 +331,10 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const double R = rows, DD = D, f4 = 4.0;
   const bool nt = P.WorbT != nullptr;
   // channel rows (local energy) take the split-bf16 GEMM unless exact-f32 is requested;
-  // the log-psi rows only in DH_GEMM_X6_ALL.  The two log-psi GEMMs that carry a LayerNorm
-  // stay on the exact-f32 gemm_ln_kernel in every mode: at 24576 x 256 x 256 it takes
-  // 42 / 47 us against 42 / 53 us for the split-bf16 form with the same epilogue
-  // (launch_gemm_x6_ln) and 33 + 16 us for split-bf16 + a separate LayerNorm launch
-  // (tools/ln_gemm_bench.py on MI355X); the short GEMMs there are epilogue/latency bound.
+  // the log-psi rows only in DH_GEMM_X6_ALL, the LayerNorm-carrying GEMMs with their
+  // LayerNorm in the split-bf16 epilogue (96-row tiles of 3 x 4 waves: 34 / 38 us at
+  // 24576 x 256 x 256 against 43 / 47 us for the exact-f32 gemm_ln_kernel;
+  // tools/ln_gemm_bench.py on MI355X)
   const bool x6 = nt && gemm_x6_supported(D) &&
                   (C > 1 ? h->gemm_mode != DH_GEMM_F32 : h->gemm_mode == DH_GEMM_X6_ALL);
   const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
@@ -371,11 +370,17 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       // log psi: each GEMM carries its LayerNorm in the epilogue, in place over h
       {
         PROF(PK_GEMM, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
-        launch_gemm_ln(w.o, D, lp.WolT, D, lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
+        if (x6)
+          launch_gemm_x6_ln(w.o, D, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
+        else
+          launch_gemm_ln(w.o, D, lp.WolT, D, lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
       }
       {
         PROF(PK_GEMM, 2.0 * R * DD * DD, f4 * (2.0 * R * DD + DD * DD));
-        launch_gemm_ln(w.h, D, lp.WmT, D, lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
+        if (x6)
+          launch_gemm_x6_ln(w.h, D, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
+        else
+          launch_gemm_ln(w.h, D, lp.WmT, D, lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
       }
       continue;
     }

@@ -89,7 +89,7 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
 void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
                     float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
 // h = LN(h + X W + b) (mode 0) or LN(h + tanh(X W + b)) (mode 1), in place, split-bf16
-// arithmetic; h [rows][256], ln = [gamma(256), beta(256)]; nw = tile height / 32 (0: pick).
+// arithmetic; h [rows][256], ln = [gamma(256), beta(256)]; nw = tile form (0: pick; gemm_x6.hip).
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s);
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).

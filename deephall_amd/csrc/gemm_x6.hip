@@ -582,22 +582,26 @@ void launch_x6c_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
 // its 32 x 256 block into LDS once, then sweeps it three times (pre-LN value + mean,
 // centred variance, normalise + store) with 16 lanes per row.  X (= h in LNM 2) is only
 // read by the DMA of this workgroup's own rows, all landed before the epilogue barrier.
-template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW))) void gemm_x6d_kernel(const float* X, int ldx,
+template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0, int WN = 1>
+__global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW * WN >= 8 ? 1 : 8 / (NW * WN)))) void gemm_x6d_kernel(const float* X, int ldx,
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
                                                        float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
                                                        int ntn, const float* __restrict__ ln) {
-  static_assert(LNM == 0 || TN == 8, "LayerNorm epilogue needs whole 256-column rows");
-  constexpr int BM = 32 * NW, BN = 32 * TN, BK = 16;
+  // NW x WN waves: wave (wm, wn) computes rows 32 wm.. and columns 32 TN wn.. of the tile
+  constexpr int NWT = NW * WN;
+  constexpr int BM = 32 * NW, BN = 32 * TN * WN, BK = 16;
+  static_assert(LNM == 0 || BN == 256, "LayerNorm epilogue needs whole 256-column rows");
+  static_assert(LNM != 0 || WN == 1, "the plain epilogue assumes one column wave");
   constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
-  constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NW - 1) / NW;
+  constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NWT - 1) / NWT;
   static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
   static_assert(ST == 2 || ST == 3, "ring depth");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
   const int l32 = lane & 31, lh = lane >> 5;
 
   const int nblk = ntm * ntn;
@@ -615,7 +619,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
   bool isA[PER];
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
-    int j = wid + t * NW;
+    int j = wid + t * NWT;
     if (j >= IA + IB) j = IA + IB - 1;  // wave-uniform: repeat the last piece
     isA[t] = j < IA;
     if (j < IA) {  // 16 rows x 64 B of f32 activations
@@ -646,11 +650,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
     }
   };
   // A fragment: row m, k = 8 lh + (0..7) = logical 16-B slots 2lh, 2lh+1 of a 64-B row
-  const int m = wid * 32 + l32;
+  const int m = wm * 32 + l32;
   const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
   const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
   // B fragment of column block j: row n = 32j + l32, slot lh ^ ((n >> 3) & 1) = lh ^ ((l32 >> 3) & 1)
-  const int boff = A_BYTES + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
+  const int boff = A_BYTES + wn * TN * 1024 + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
 
   f32x16 acc[TN];
 #pragma unroll
@@ -786,95 +790,70 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
   // writes whole 256-B row pieces with global_store_dwordx4 (4 rows per instruction; the
   // residual is read the same way).  dword stores of the MFMA layout were store-issue bound.
   __syncthreads();  // every wave is done with the ring buffers
-  const int rw0 = row0 + wid * 32;
   if constexpr (LNM != 0) {
-    constexpr int LS = 260;  // row stride (floats): conflict-free ds_write_b128, as 68 below
-    float* blk = reinterpret_cast<float*>(smem) + wid * (32 * LS);
+    // every wave puts its 32 x 32TN block into the shared [BM][LS] tile (row stride 260:
+    // conflict-free ds_write_b128, as 68 below); then each wave normalises whole rows
+    // wid, wid + NWT, ...: 64 lanes x 4 columns, row statistics by wave reduction
+    // (two-pass mean / centred variance, eps 1e-5, as gemm_ln_kernel)
+    constexpr int LS = 260;
+    float* blk = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(blk + l32 * LS + 32 * j + 8 * g + 4 * lh) =
+        *reinterpret_cast<float4*>(blk + (32 * wm + l32) * LS + 32 * (wn * TN + j) + 8 * g + 4 * lh) =
             make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
-    const int lr = lane >> 4, lc = (lane & 15) * 4;  // rows 4q + lr, columns 64p + lc .. +3
-    float mean[8], rstd[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) mean[q] = 0.f;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int c = 64 * p + lc;
-      const float4 bv = *reinterpret_cast<const float4*>(bias + c);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int rr = 4 * q + lr, r = rw0 + rr;
-        float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
-        v.x += bv.x;
-        v.y += bv.y;
-        v.z += bv.z;
-        v.w += bv.w;
-        if (LNM == 2) {
-          v.x = tanhf(v.x);
-          v.y = tanhf(v.y);
-          v.z = tanhf(v.z);
-          v.w = tanhf(v.w);
-        }
-        if (r < rows) {
-          const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
-          v.x += rv.x;
-          v.y += rv.y;
-          v.z += rv.z;
-          v.w += rv.w;
-        }
-        *reinterpret_cast<float4*>(blk + rr * LS + c) = v;
-        mean[q] += (v.x + v.y) + (v.z + v.w);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float t = mean[q];
+    __syncthreads();
+    const int c = 4 * lane;
+    const float4 bv = *reinterpret_cast<const float4*>(bias + c);
+    const float4 gm = *reinterpret_cast<const float4*>(ln + c);
+    const float4 bt = *reinterpret_cast<const float4*>(ln + 256 + c);
+    auto wsum = [](float t) {
       t += __shfl_xor(t, 1, 64);
       t += __shfl_xor(t, 2, 64);
       t += __shfl_xor(t, 4, 64);
       t += __shfl_xor(t, 8, 64);
-      mean[q] = t * (1.f / 256.f);
-      rstd[q] = 0.f;
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(blk + (4 * q + lr) * LS + 64 * p + lc);
-        const float dx = v.x - mean[q], dy = v.y - mean[q], dz = v.z - mean[q], dw = v.w - mean[q];
-        rstd[q] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      return t;
+    };
+    for (int rr = wid; rr < BM; rr += NWT) {
+      const int r = row0 + rr;
+      float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
+      v.x += bv.x;
+      v.y += bv.y;
+      v.z += bv.z;
+      v.w += bv.w;
+      if (LNM == 2) {
+        v.x = tanhf(v.x);
+        v.y = tanhf(v.y);
+        v.z = tanhf(v.z);
+        v.w = tanhf(v.w);
       }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float t = rstd[q];
-      t += __shfl_xor(t, 1, 64);
-      t += __shfl_xor(t, 2, 64);
-      t += __shfl_xor(t, 4, 64);
-      t += __shfl_xor(t, 8, 64);
-      rstd[q] = 1.f / sqrtf(t * (1.f / 256.f) + 1e-5f);
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int c = 64 * p + lc;
-      const float4 gm = *reinterpret_cast<const float4*>(ln + c);
-      const float4 bt = *reinterpret_cast<const float4*>(ln + 256 + c);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int rr = 4 * q + lr, r = rw0 + rr;
-        const float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
-        float4 o;
-        o.x = gm.x * (rstd[q] * (v.x - mean[q])) + bt.x;
-        o.y = gm.y * (rstd[q] * (v.y - mean[q])) + bt.y;
-        o.z = gm.z * (rstd[q] * (v.z - mean[q])) + bt.z;
-        o.w = gm.w * (rstd[q] * (v.w - mean[q])) + bt.w;
-        if (r < rows) *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = o;
+      if (r < rows) {
+        const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+        v.x += rv.x;
+        v.y += rv.y;
+        v.z += rv.z;
+        v.w += rv.w;
       }
+      const float mean = wsum((v.x + v.y) + (v.z + v.w)) * (1.f / 256.f);
+      v.x -= mean;
+      v.y -= mean;
+      v.z -= mean;
+      v.w -= mean;
+      const float var = wsum((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w)) * (1.f / 256.f);
+      const float rs = 1.f / sqrtf(var + 1e-5f);
+      float4 o;
+      o.x = gm.x * (rs * v.x) + bt.x;
+      o.y = gm.y * (rs * v.y) + bt.y;
+      o.z = gm.z * (rs * v.z) + bt.z;
+      o.w = gm.w * (rs * v.w) + bt.w;
+      if (r < rows) *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = o;
     }
     return;
   }
+  const int rw0 = row0 + wid * 32;
   float* red = reinterpret_cast<float*>(smem) + wid * (32 * 68);
   const bool full = rw0 + 32 <= rows && col0 + BN <= ncols;
   const int lr = lane >> 4, lc = (lane & 15) * 4;  // read-back: rows 4q + lr, columns lc..lc+3
@@ -939,18 +918,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8 / NW)
   }
 }
 
-template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0>
+template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0, int WN = 1>
 void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
                   float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, const float* ln = nullptr) {
-  constexpr int BM = 32 * NW, BN = 32 * TN;
+  constexpr int BM = 32 * NW, BN = 32 * TN * WN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
   // LDS: the DMA ring, reused by the epilogue's per-wave 32 x 68-float transpose regions
-  // (32 x 260 floats, whole rows, with the LayerNorm epilogue)
+  // (a shared BM x 260-float tile of whole rows with the LayerNorm epilogue)
   const size_t smem =
-      std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)NW * 32 * (LNM ? 260 : 68) * 4);
-  ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST, LNM>, smem);
-  hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST, LNM>), dim3(ntm * ntn), dim3(NW * 64), smem, s, X, ldx, Wp,
-                     ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln);
+      std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)(LNM ? BM * 260 : NW * 32 * 68) * 4);
+  ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>, smem);
+  hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>), dim3(ntm * ntn), dim3(NW * WN * 64), smem, s, X,
+                     ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln);
 }
 
 // ---- persistent lean form: one DMA ring across all of a workgroup's tiles --------------------
@@ -1517,23 +1496,28 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
 }
 
 
-// log-psi GEMM + LayerNorm (LNM 1 / 2 above), in place over h [rows][256].  Tile height
-// 32 * nw rows (nw 3 or 4; 0 = choose): one workgroup per CU (LDS), so the height is picked
-// to fill the CUs with the fewest tile rounds; callers pad rows to 256 and a tile never
-// reads X past round_up(rows, 256).
+// log-psi GEMM + LayerNorm (LNM 1 / 2 above), in place over h [rows][256].  Form nw:
+//   0 = choose; 3 / 4 = 96 / 128-row tiles of 32 x 256 wave blocks (3 / 4 waves);
+//   1 = 96-row tiles of 3 x 4 waves with 32 x 64 blocks (12 waves, all four SIMDs busy);
+//   2 = 64-row tiles of 2 x 4 waves.
+// One workgroup per CU (LDS).  Callers pad rows to 256; a tile never reads X past
+// round_up(rows, 256) (96-row tiles only when round_up(rows, 96) stays inside).
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s) {
-  if (nw != 3 && nw != 4) {
-    const int cu = cu_count_x6();
-    auto cost = [&](int w) { return ((rows + 32 * w - 1) / (32 * w) + cu - 1) / cu * w; };
-    nw = (cost(3) < cost(4) && round_up(rows, 96) <= round_up(rows, 256)) ? 3 : 4;
-  }
-#define DH_X6LN(NWV, M) \
-  launch_x6d_t<8, 0, NWV, 3, M>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln)
-  if (nw == 3) {
-    if (mode == 0) DH_X6LN(3, 1); else DH_X6LN(3, 2);
-  } else {
-    if (mode == 0) DH_X6LN(4, 1); else DH_X6LN(4, 2);
+  const bool r96 = round_up(rows, 96) <= round_up(rows, 256);
+  if (nw < 1 || nw > 4 || (!r96 && (nw == 1 || nw == 3))) nw = r96 ? 1 : 2;
+#define DH_X6LN(TNV, NWV, WNV)                                                                              \
+  do {                                                                                                      \
+    if (mode == 0)                                                                                          \
+      launch_x6d_t<TNV, 0, NWV, 3, 1, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln); \
+    else                                                                                                    \
+      launch_x6d_t<TNV, 0, NWV, 3, 2, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln); \
+  } while (0)
+  switch (nw) {
+    case 1: DH_X6LN(2, 3, 4); break;
+    case 2: DH_X6LN(2, 2, 4); break;
+    case 3: DH_X6LN(8, 3, 1); break;
+    default: DH_X6LN(8, 4, 1);
   }
 #undef DH_X6LN
 }

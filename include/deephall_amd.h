@@ -109,9 +109,8 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
  *                 six bf16 products per pair (dropped terms <= 2^-24 |ab|, f32 accumulate);
  *                 error at the level of the f32 GEMM (tests/test_gpu_kernels.py), 2.67x the
  *                 f32 matrix rate.
- *   DH_GEMM_X6_ALL  split-bf16 also for the log-psi / MCMC GEMMs without a LayerNorm
- *                 epilogue (q|k|v, orbitals); the LayerNorm-carrying ones stay exact-f32
- *                 (measured faster at log-psi row counts).  Default.
+ *   DH_GEMM_X6_ALL  split-bf16 also for the log-psi / MCMC GEMMs (the two per layer that
+ *                 carry a LayerNorm with it in their epilogue).  Default.
  * In DH_GEMM_F32 and DH_GEMM_X6 the log-psi / MCMC passes use the exact-f32 kernels. */
 #define DH_GEMM_F32 0
 #define DH_GEMM_X6 1
@@ -203,7 +202,8 @@ int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt,
                      const float* ln, float* h, int rows, int K, void* stream);
 
 /* Split-bf16 form of dh_debug_gemm_ln (weight as the planes of dh_debug_split_planes,
- * ldp >= dh_debug_x6_plane_rows(256)); nw = tile height / 32: 3, 4 or 0 (choose). */
+ * ldp >= dh_debug_x6_plane_rows(256)); nw = tile form: 1 = 96 rows x (3 x 4 waves),
+ * 2 = 64 rows x (2 x 4 waves), 3 / 4 = 96 / 128 rows of whole-row waves, 0 = choose. */
 int dh_debug_gemm_x6_ln(int mode, int nw, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
                         const float* ln, float* h, int rows, int K, void* stream);
 

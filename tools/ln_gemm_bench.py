@@ -51,7 +51,7 @@ flops = 2.0 * rows * D * K
 for v in (-1, 43, 44, 45, 46, 40):
     us = timed(lambda: lib.dh_debug_gemm_x6(v, p(X), K, p(Wp), ldp, p(b), p(h), D, p(Y), D, rows, D, K, 1, s))
     print(f"x6 gemm variant {v:3d}: {us:7.1f} us  {flops / us / 1e6:6.1f} TF/s")
-for nw in (3, 4):
+for nw in (1, 2, 3, 4):
     for mode in (0, 1):
         us = timed(lambda: lib.dh_debug_gemm_x6_ln(mode, nw, p(X), K, p(Wp), ldp, p(b), p(ln), p(h), rows, K, s))
         print(f"x6 gemm+LN nw={nw} mode={mode}: {us:7.1f} us  {flops / us / 1e6:6.1f} TF/s")
