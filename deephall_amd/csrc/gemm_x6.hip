@@ -592,7 +592,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   constexpr int NWT = NW * WN;
   constexpr int BM = 32 * NW, BN = 32 * TN * WN, BK = 16;
   static_assert(LNM == 0 || BN == 256, "LayerNorm epilogue needs whole 256-column rows");
-  static_assert(LNM != 0 || WN == 1, "the plain epilogue assumes one column wave");
+  static_assert(WN == 1 || BN == 256, "shared-tile epilogue: 64 lanes x 4 columns");
   constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
   constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NWT - 1) / NWT;
   static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
@@ -853,6 +853,43 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
     }
     return;
   }
+  if constexpr (WN > 1) {
+    // plain epilogue of the 2-D wave grid: the same shared tile, then whole 1-KB row
+    // pieces per wave instruction (ncols % 4 == 0: a float4 is in or out as a whole)
+    constexpr int LS = 260;
+    float* blk = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(blk + (32 * wm + l32) * LS + 32 * (wn * TN + j) + 8 * g + 4 * lh) =
+            make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
+    __syncthreads();
+    const int c = col0 + 4 * lane;
+    if (c >= ncols) return;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias) bv = *reinterpret_cast<const float4*>(bias + c);
+    for (int rr = wid; rr < BM; rr += NWT) {
+      const int r = row0 + rr;
+      if (r >= rows) break;
+      float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + 4 * lane);
+      if (bias && (C == 1 || r % C == 0)) {
+        v.x += bv.x;
+        v.y += bv.y;
+        v.z += bv.z;
+        v.w += bv.w;
+      }
+      if (R) {
+        const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+        v.x += rv.x;
+        v.y += rv.y;
+        v.z += rv.z;
+        v.w += rv.w;
+      }
+      *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = v;
+    }
+    return;
+  }
   const int rw0 = row0 + wid * 32;
   float* red = reinterpret_cast<float*>(smem) + wid * (32 * 68);
   const bool full = rw0 + 32 <= rows && col0 + BN <= ncols;
@@ -924,9 +961,9 @@ void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
   constexpr int BM = 32 * NW, BN = 32 * TN * WN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
   // LDS: the DMA ring, reused by the epilogue's per-wave 32 x 68-float transpose regions
-  // (a shared BM x 260-float tile of whole rows with the LayerNorm epilogue)
+  // (a shared BM x 260-float tile of whole rows with the LayerNorm epilogue or WN > 1)
   const size_t smem =
-      std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)(LNM ? BM * 260 : NW * 32 * 68) * 4);
+      std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)(LNM || WN > 1 ? BM * 260 : NW * 32 * 68) * 4);
   ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>, smem);
   hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>), dim3(ntm * ntn), dim3(NW * WN * 64), smem, s, X,
                      ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln);
@@ -1453,6 +1490,21 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
       break;
     case 46:
       launch_x6d_t<4, 0, 8, 2>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    // 2-D wave grids, 256-column tiles (ncols % 4 == 0): 96 x 256 of 3 x 4 waves (when
+    // round_up(rows, 96) stays inside round_up(rows, 256), else 64 x 256), 64 x 256 of
+    // 2 x 4 waves, 128 x 256 of 4 x 4 waves
+    case 60:
+      if (round_up(rows, 96) <= round_up(rows, 256)) {
+        launch_x6d_t<2, 0, 3, 3, 0, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+        break;
+      }
+      [[fallthrough]];
+    case 61:
+      launch_x6d_t<2, 0, 2, 3, 0, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 62:
+      launch_x6d_t<2, 0, 4, 3, 0, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
     // persistent lean
     case 50:

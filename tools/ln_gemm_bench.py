@@ -48,9 +48,17 @@ def timed(fn, reps=50):
 
 
 flops = 2.0 * rows * D * K
-for v in (-1, 43, 44, 45, 46, 40):
-    us = timed(lambda: lib.dh_debug_gemm_x6(v, p(X), K, p(Wp), ldp, p(b), p(h), D, p(Y), D, rows, D, K, 1, s))
-    print(f"x6 gemm variant {v:3d}: {us:7.1f} us  {flops / us / 1e6:6.1f} TF/s")
+for n in (256, 768, 192):
+    Wn = torch.randn(K, n, device="cuda") / 16
+    ldn = lib.dh_debug_x6_plane_rows(n)
+    Wpn = torch.empty(3 * ldn * K, dtype=torch.int16, device="cuda")
+    assert lib.dh_debug_split_planes(p(Wn.t().contiguous()), K, n, K, p(Wpn), s) == 0
+    bn = torch.randn(n, device="cuda")
+    Yn = torch.empty(rp, n, device="cuda")
+    fl = 2.0 * rows * n * K
+    for v in (-1, 44, 46, 60, 61, 62):
+        us = timed(lambda: lib.dh_debug_gemm_x6(v, p(X), K, p(Wpn), ldn, p(bn), None, n, p(Yn), n, rows, n, K, 1, s))
+        print(f"x6 gemm {rows}x{n}x{K} variant {v:3d}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s")
 for nw in (1, 2, 3, 4):
     for mode in (0, 1):
         us = timed(lambda: lib.dh_debug_gemm_x6_ln(mode, nw, p(X), K, p(Wp), ldp, p(b), p(ln), p(h), rows, K, s))
