@@ -1538,12 +1538,14 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
                     float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   // measured on MI355X (tools/gemm_bench.py, K = 256): channel rows take the persistent lean
   // kernel with 256 x 256 tiles (256 x 192 when ncols is a multiple of 192 only); short
-  // (log-psi) row counts take 256 x 128 tiles, two workgroups per CU.
+  // (log-psi) row counts take 256 x 128 tiles, two workgroups per CU (128 x 192 when ncols
+  // is a multiple of 192: q|k|v 24576 x 768 in 64 vs 68 us).  The 2-D wave grids (60-62)
+  // were no faster at these shapes (tools/ln_gemm_bench.py).
   int v;
   if (rows >= 65536)
     v = (ncols % 192 == 0 && ncols % 256 != 0) ? 51 : 50;
   else
-    v = (ncols % 192 == 0 && ncols % 256 != 0) ? 44 : 46;
+    v = (ncols % 192 == 0) ? 44 : 46;
   launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
 }
 
