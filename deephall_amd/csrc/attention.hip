@@ -1050,7 +1050,10 @@ void launch_ch(const Dims& d, const float* qkv, const float* geo, float* o, int 
 
 }  // namespace
 
-bool attention_takes_features(const Dims& d) { return d.dh == 64 && d.N <= 8; }
+// wave kernels: every N <= 8, plus the N = 10 and N = 20 instances of BASELINE.json's
+// C4 / C5 configs (one wave per (walker, head) there too: 2x / 10x faster than the
+// 256-thread channel kernel v2, whose three barriers per channel dominate)
+bool attention_takes_features(const Dims& d) { return d.dh == 64 && (d.N <= 8 || d.N == 10 || d.N == 20); }
 
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
                       const float* W0qkv, const float* bqkv) {
@@ -1065,7 +1068,9 @@ void launch_attention(const Dims& d, const float* qkv, const float* geo, float* 
       case 5: launch_wave<5>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
       case 6: launch_wave<6>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
       case 7: launch_wave<7>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      default: launch_wave<8>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 8: launch_wave<8>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 10: launch_wave<10>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      default: launch_wave<20>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
     }
   }
   // channel kernel v2 needs dh <= 64 (one feature column per lane) and dh % 4 == 0;
