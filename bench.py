@@ -61,9 +61,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
+    # DH_BENCH_BACKEND=gloo, DH_BENCH_ONE_GPU=1 puts every rank on device 0
+    if os.environ.get("DH_BENCH_ONE_GPU"):
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("DH_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
 
     from deephall_amd import _lib, config
