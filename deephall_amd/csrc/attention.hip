@@ -646,8 +646,13 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
                                                             const float* __restrict__ bqkv, int n_up) {
   constexpr int dh = 64, ld = 68, T = 2 * N, C = 2 * N + 5, nn = N * N;
   extern __shared__ float sm[];
-  float *q0 = sm, *k0 = q0 + N * ld, *v0 = k0 + N * ld, *qc = v0 + N * ld, *kc = qc + N * ld, *vc = kc + N * ld;
-  float *A0 = vc + N * ld, *S = A0 + nn, *P = S + nn, *Rm = P + nn, *accS = Rm + nn, *T2 = accS + nn;
+  // VR (N > 8): v of the value channel and of the current channel live in registers
+  // (lane = column), which frees 2 N x 68 floats of LDS per wave (C5: 61 vs 88 ms per
+  // step); for N <= 8 the LDS copy keeps the register count down (C2: 1.0 vs 1.27 ms)
+  constexpr bool VR = N > 8;
+  constexpr int NV = VR ? 0 : N * ld;
+  float *q0 = sm, *k0 = q0 + N * ld, *v0 = k0 + N * ld, *qc = v0 + NV, *kc = qc + N * ld, *vc = kc + N * ld;
+  float *A0 = vc + NV, *S = A0 + nn, *P = S + nn, *Rm = P + nn, *accS = Rm + nn, *T2 = accS + nn;
   float *SuB = T2 + nn, *Au = SuB + 3 * nn, *QK = Au + 3 * nn, *al = QK + 3 * nn;
   const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H, lane = threadIdx.x;
   const int D = H * dh;
@@ -672,7 +677,8 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
       }
     }
   };
-  auto commit = [&](float* qd, float* kd, float* vd) {
+  float v0reg[VR ? N : 1], vcreg[VR ? N : 1];
+  auto commit = [&](float* qd, float* kd, float* vl, float* vr) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       if constexpr (FEAT) {
@@ -681,11 +687,18 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
         const bool v = pending == 0;
         qd[i * ld + lane] = FeatW::dot(f, fw.wq) + (v ? fw.bq : 0.f);
         kd[i * ld + lane] = FeatW::dot(f, fw.wk) + (v ? fw.bk : 0.f);
-        vd[i * ld + lane] = FeatW::dot(f, fw.wv) + (v ? fw.bv : 0.f);
+        const float vv = FeatW::dot(f, fw.wv) + (v ? fw.bv : 0.f);
+        if constexpr (VR)
+          vr[i] = vv;
+        else
+          vl[i * ld + lane] = vv;
       } else {
         qd[i * ld + lane] = pq[i];
         kd[i * ld + lane] = pk[i];
-        vd[i * ld + lane] = pv[i];
+        if constexpr (VR)
+          vr[i] = pv[i];
+        else
+          vl[i * ld + lane] = pv[i];
       }
     }
   };
@@ -717,7 +730,7 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
     }
   }
   prefetch(0);
-  commit(q0, k0, v0);
+  commit(q0, k0, v0, v0reg);
   prefetch(1);
   for (int p = lane; p < nn; p += 64) {
     accS[p] = 0.f;
@@ -753,7 +766,7 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
   {
     float v0r[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) v0r[j] = v0[j * ld + lane];
+    for (int j = 0; j < N; ++j) v0r[j] = VR ? v0reg[VR ? j : 0] : v0[j * ld + lane];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       float acc = 0.f;
@@ -786,7 +799,7 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
 
   for (int c = 1; c < C; ++c) {
     wsync();
-    commit(qc, kc, vc);
+    commit(qc, kc, vc, vcreg);
     if (c + 1 < C) prefetch(c + 1);
     wsync();
     const bool tang = c <= T;
@@ -848,8 +861,8 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
       float v0r[N], vcr[N];
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        v0r[j] = v0[j * ld + lane];
-        vcr[j] = vc[j * ld + lane];
+        v0r[j] = VR ? v0reg[VR ? j : 0] : v0[j * ld + lane];
+        vcr[j] = VR ? vcreg[VR ? j : 0] : vc[j * ld + lane];
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) {
@@ -1031,7 +1044,7 @@ void launch_wave(const Dims& d, const float* qkv, const float* W0qkv, const floa
                          d.H, ntask, W0qkv, bqkv, d.n_up);
     return;
   }
-  const size_t smem = (size_t)(6 * N * 68 + 15 * nn + 6 * N) * sizeof(float);
+  const size_t smem = (size_t)((N > 8 ? 4 : 6) * N * 68 + 15 * nn + 6 * N) * sizeof(float);  // VR above
   if (W0qkv)
     hipLaunchKernelGGL((attention_wave_kernel<N, true>), dim3(nw * d.H), dim3(64), smem, s, qkv, geo, o, d.H, W0qkv,
                        bqkv, d.n_up);
