@@ -352,11 +352,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // the attention kernel when it supports that (fused), else written by the input kernel.
   const bool fold = d.L > 0;
   const bool fused = fold && attention_takes_features(d);
+  // log psi, split-bf16: layer 1's residual h = features W0 is formed in the epilogue of
+  // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
+  const bool h_feat = C == 1 && fused && x6 && ln_fused;
   {
     const bool wq = fold && !fused;
     PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
-    launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, w.h, wq ? w.qkv : nullptr,
-                 w.geo, nw, C, s);
+    launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, h_feat ? nullptr : w.h,
+                 wq ? w.qkv : nullptr, w.geo, nw, C, s);
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
@@ -371,7 +374,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       {
         PROF(PK_GEMM, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
         if (x6)
-          launch_gemm_x6_ln(w.o, D, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
+          launch_gemm_x6_ln(w.o, D, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.h, rows, D, 0, 0, s,
+                            (h_feat && l == 0) ? X6Feat{P.W0, w.geo, d.N, d.n_up} : X6Feat{});
         else
           launch_gemm_ln(w.o, D, lp.WolT, D, lp.bol, lp.ln1, w.h, rows, D, 0, 0, s);
       }

@@ -587,7 +587,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
                                                        float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
-                                                       int ntn, const float* __restrict__ ln) {
+                                                       int ntn, const float* __restrict__ ln, X6Feat feat) {
   // NW x WN waves: wave (wm, wn) computes rows 32 wm.. and columns 32 TN wn.. of the tile
   constexpr int NWT = NW * WN;
   constexpr int BM = 32 * NW, BN = 32 * TN * WN, BK = 16;
@@ -808,6 +808,11 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
     const float4 bv = *reinterpret_cast<const float4*>(bias + c);
     const float4 gm = *reinterpret_cast<const float4*>(ln + c);
     const float4 bt = *reinterpret_cast<const float4*>(ln + 256 + c);
+    float4 w0[4];  // residual from the features (feat.W0): input.hip's h = f W0, same order
+    if (feat.W0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w0[q] = *reinterpret_cast<const float4*>(feat.W0 + q * 256 + c);
+    }
     auto wsum = [](float t) {
       t += __shfl_xor(t, 1, 64);
       t += __shfl_xor(t, 2, 64);
@@ -831,7 +836,17 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
         v.w = tanhf(v.w);
       }
       if (r < rows) {
-        const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+        float4 rv;
+        if (feat.W0) {
+          const float4 g = *reinterpret_cast<const float4*>(feat.geo + 4 * (size_t)r);  // st ct sp cp
+          const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (r % feat.N < feat.n_up) ? 1.f : -1.f);
+          rv.x = f.x * w0[0].x + f.y * w0[1].x + f.z * w0[2].x + f.w * w0[3].x;
+          rv.y = f.x * w0[0].y + f.y * w0[1].y + f.z * w0[2].y + f.w * w0[3].y;
+          rv.z = f.x * w0[0].z + f.y * w0[1].z + f.z * w0[2].z + f.w * w0[3].z;
+          rv.w = f.x * w0[0].w + f.y * w0[1].w + f.z * w0[2].w + f.w * w0[3].w;
+        } else {
+          rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+        }
         v.x += rv.x;
         v.y += rv.y;
         v.z += rv.z;
@@ -957,7 +972,8 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
 
 template <int TN, int ABL = 0, int NW = 8, int ST = 3, int LNM = 0, int WN = 1>
 void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
-                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, const float* ln = nullptr) {
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, const float* ln = nullptr,
+                  X6Feat feat = X6Feat{}) {
   constexpr int BM = 32 * NW, BN = 32 * TN * WN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
   // LDS: the DMA ring, reused by the epilogue's per-wave 32 x 68-float transpose regions
@@ -966,7 +982,7 @@ void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
       std::max((size_t)ST * (BM * 16 * 4 + 3 * BN * 16 * 2), (size_t)(LNM || WN > 1 ? BM * 260 : NW * 32 * 68) * 4);
   ensure_smem(gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>, smem);
   hipLaunchKernelGGL((gemm_x6d_kernel<TN, ABL, NW, ST, LNM, WN>), dim3(ntm * ntn), dim3(NW * WN * 64), smem, s, X,
-                     ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln);
+                     ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn, ln, feat);
 }
 
 // ---- persistent lean form: one DMA ring across all of a workgroup's tiles --------------------
@@ -1557,13 +1573,14 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
 // One workgroup per CU (LDS).  Callers pad rows to 256; a tile never reads X past
 // round_up(rows, 256) (96-row tiles only when round_up(rows, 96) stays inside).
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                       float* h, int rows, int K, int mode, int nw, hipStream_t s) {
+                       float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat) {
+  if (mode != 0) feat = X6Feat{};
   const bool r96 = round_up(rows, 96) <= round_up(rows, 256);
   if (nw < 1 || nw > 4 || (!r96 && (nw == 1 || nw == 3))) nw = r96 ? 1 : 2;
 #define DH_X6LN(TNV, NWV, WNV)                                                                              \
   do {                                                                                                      \
     if (mode == 0)                                                                                          \
-      launch_x6d_t<TNV, 0, NWV, 3, 1, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln); \
+      launch_x6d_t<TNV, 0, NWV, 3, 1, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln, feat); \
     else                                                                                                    \
       launch_x6d_t<TNV, 0, NWV, 3, 2, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln); \
   } while (0)

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x,
     }
     F[tid] = f;
   }
+  if (!h && !qkv) return;  // geometry only (the log-psi layer-1 residual is formed later)
   __syncthreads();
   const int nr = min(kRows, rows - row0);
   for (int q = tid; q < nr * E4; q += blockDim.x) {
