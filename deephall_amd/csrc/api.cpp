@@ -339,11 +339,10 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
                   (C > 1 ? h->gemm_mode != DH_GEMM_F32 : h->gemm_mode == DH_GEMM_X6_ALL);
   const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
   auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, const uint16_t* Wp, int ldw,
-                  const float* bias, const float* Res, int ldr, float* Y, int ldy, int ncols, int K,
-                  X6Feat feat = X6Feat{}) {
+                  const float* bias, const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
     PROF(PK_GEMM + (C > 1 ? PK_CH : 0), 2.0 * R * ncols * K, f4 * (R * K + (double)K * ncols + R * ncols * (Res ? 2 : 1)));
     if (x6)
-      launch_gemm_x6(X, ldx, Wp, x6_plane_rows(ncols), bias, Res, ldr, Y, ldy, rows, ncols, K, C, s, feat);
+      launch_gemm_x6(X, ldx, Wp, x6_plane_rows(ncols), bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
     else if (nt)
       launch_gemm_nt(X, ldx, Wt, K, bias, Res, ldr, Y, ldy, rows, ncols, K, C, s);
     else
@@ -355,7 +354,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const bool fused = fold && attention_takes_features(d);
   // log psi, split-bf16: layer 1's residual h = features W0 is formed in the epilogue of
   // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
-  const bool h_feat = fused && x6 && (C == 1 ? ln_fused : gemm_x6_takes_features(rows));
+  const bool h_feat = C == 1 && fused && x6 && ln_fused;
   {
     const bool wq = fold && !fused;
     PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
@@ -390,8 +389,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       continue;
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
-    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, w.h, D, w.t, D, D, D,
-         (h_feat && l == 0) ? X6Feat{P.W0, w.geo, d.N, d.n_up} : X6Feat{});
+    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, w.h, D, w.t, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
       launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);

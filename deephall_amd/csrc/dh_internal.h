@@ -83,22 +83,20 @@ void launch_gemm_ln(const float* X, int ldx, const float* Wt, int ldw, const flo
 int x6_plane_rows(int ncols);
 void launch_split_planes(const float* Wt, int ldw, int ncols, int K, uint16_t* Wp, hipStream_t s);
 bool gemm_x6_supported(int K);
-// feat (layer 1): the residual h = features W0 is formed in the GEMM epilogue from geo
-// [walker*N + electron][4] = (sin th, cos th, sin ph, cos ph) and W0 [4][ldr] instead of read
-// (log-psi LayerNorm GEMM; channel GEMMs when gemm_x6_takes_features(rows)).
+void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
+                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
+                            hipStream_t s);
+void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s);
+// h = LN(h + X W + b) (mode 0) or LN(h + tanh(X W + b)) (mode 1), in place, split-bf16
+// arithmetic; h [rows][256], ln = [gamma(256), beta(256)]; nw = tile form (0: pick; gemm_x6.hip).
+// feat (layer 1 of log psi, mode 0): the residual h = features W0 is formed in the epilogue
+// from geo [rows][4] = (sin th, cos th, sin ph, cos ph) and W0 [4][256] instead of read.
 struct X6Feat {
   const float* W0 = nullptr;
   const float* geo = nullptr;
   int N = 1, n_up = 0;
 };
-void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
-                            const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
-                            hipStream_t s, X6Feat feat = X6Feat{});
-bool gemm_x6_takes_features(int rows);
-void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
-                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, X6Feat feat = X6Feat{});
-// h = LN(h + X W + b) (mode 0) or LN(h + tanh(X W + b)) (mode 1), in place, split-bf16
-// arithmetic; h [rows][256], ln = [gamma(256), beta(256)]; nw = tile form (0: pick; gemm_x6.hip).
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).

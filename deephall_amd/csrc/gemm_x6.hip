@@ -992,39 +992,12 @@ void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
 // transposes through its own LDS region (not the ring) and its 4*TN dwordx4 stores stay
 // in flight under the next steps (counted: vmcnt(4*TN) at the next step's wait; VMEM ops of
 // a wave complete in order).  LDS: ring 3 x 40 KiB + 8 x 4.5 KiB transpose = 156 KiB.
-// input-feature channel of channel row r (rows (walker, electron, channel), C channels):
-// the seeds of input.hip, [z, x, y, spin] order of psiformer.py:51-60
-__device__ __forceinline__ float4 x6_feature_row(int r, int C, const X6Feat& f) {
-  const int e = r / C, c = r - e * C, i = e % f.N, T = 2 * f.N;
-  const float4 g = *reinterpret_cast<const float4*>(f.geo + 4 * (size_t)e);  // st ct sp cp
-  const float st = g.x, ct = g.y, sp = g.z, cp = g.w;
-  const float rx = st * cp, ry = st * sp, rz = ct;
-  if (c == 0) return make_float4(rz, rx, ry, (i < f.n_up) ? 1.f : -1.f);
-  if (c <= T) {
-    const int t = c - 1;
-    if ((t >> 1) != i) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
-  }
-  if (c == T + 1) return make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
-  const int k = c - T - 2;  // 0:x 1:y 2:z
-  return make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
-}
-// f W0 for four consecutive columns (w_q = row q of W0), input.hip's order of operations
-__device__ __forceinline__ float4 x6_feature_dot(float4 f, float4 w0, float4 w1, float4 w2, float4 w3) {
-  float4 o;
-  o.x = f.x * w0.x + f.y * w1.x + f.z * w2.x + f.w * w3.x;
-  o.y = f.x * w0.y + f.y * w1.y + f.z * w2.y + f.w * w3.y;
-  o.z = f.x * w0.z + f.y * w1.z + f.z * w2.z + f.w * w3.z;
-  o.w = f.x * w0.w + f.y * w1.w + f.z * w2.w + f.w * w3.w;
-  return o;
-}
-
 template <int TN, bool HAS_R>
 __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__ X, int ldx,
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
                                                        float* Y, int ldy, int rows, int ncols, int K, int C, int ntm,
-                                                       int ntn, X6Feat feat) {
+                                                       int ntn) {
   constexpr int NW = 8, BM = 256, BN = 32 * TN, BK = 16;
   constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
   constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NW - 1) / NW;
@@ -1192,24 +1165,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
       for (int j = 0; j < TN; ++j)  // vq == 0 without a bias: the zeros are never added
         bvv[j] = bias ? *reinterpret_cast<const float4*>(bias + col0 + 32 * j + lc) : make_float4(0.f, 0.f, 0.f, 0.f);
       float4 rcur[4], rnext[4];
-      // feat.W0 (layer-1 channel rows): the residual h = f W0 is formed from the lane's four
-      // rows' input-feature channels instead of read (input.hip then writes geometry only)
-      float4 fq[4];
-      if (HAS_R && feat.W0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) fq[q] = x6_feature_row(rw0 + 8 * q + lr, C, feat);
-      }
       auto load_r = [&](int j, float4(&dst)[4]) {
-        if (feat.W0) {
-          const int cc = col0 + 32 * j + lc;
-          const float4 w0 = *reinterpret_cast<const float4*>(feat.W0 + cc);
-          const float4 w1 = *reinterpret_cast<const float4*>(feat.W0 + ldr + cc);
-          const float4 w2 = *reinterpret_cast<const float4*>(feat.W0 + 2 * ldr + cc);
-          const float4 w3 = *reinterpret_cast<const float4*>(feat.W0 + 3 * ldr + cc);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dst[q] = x6_feature_dot(fq[q], w0, w1, w2, w3);
-          return;
-        }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           dst[q] = *reinterpret_cast<const float4*>(R + (size_t)(rw0 + 8 * q + lr) * ldr + col0 + 32 * j + lc);
@@ -1261,20 +1217,10 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
           const int rr = 8 * q + lr, r = rw0 + rr;
           if (r >= rows) continue;
           const float* x4 = red + rr * TS + lc;
-          float4 fr = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (HAS_R && feat.W0) fr = x6_feature_row(r, C, feat);
           for (int t2 = 0; t2 < 4 && c + t2 < ncols; ++t2) {
             float x = x4[t2];
             if (vq & (1u << q)) x += bias[c + t2];
-            if (HAS_R) {
-              if (feat.W0) {
-                const int cc = c + t2;
-                x += fr.x * feat.W0[cc] + fr.y * feat.W0[ldr + cc] + fr.z * feat.W0[2 * ldr + cc] +
-                     fr.w * feat.W0[3 * ldr + cc];
-              } else {
-                x += R[(size_t)r * ldr + c + t2];
-              }
-            }
+            if (HAS_R) x += R[(size_t)r * ldr + c + t2];
             Y[(size_t)r * ldy + c + t2] = x;
           }
         }
@@ -1288,7 +1234,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
 
 template <int TN>
 void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
-                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, X6Feat feat = X6Feat{}) {
+                  float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   constexpr int BM = 256, BN = 32 * TN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
   const size_t smem = 3ull * (BM * 16 * 4 + 3 * BN * 16 * 2) + 8ull * 32 * 36 * 4;
@@ -1297,11 +1243,11 @@ void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
   if (R) {
     ensure_smem(gemm_x6q_kernel<TN, true>, smem);
     hipLaunchKernelGGL((gemm_x6q_kernel<TN, true>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
-                       ldy, rows, ncols, K, C, ntm, ntn, feat);
+                       ldy, rows, ncols, K, C, ntm, ntn);
   } else {
     ensure_smem(gemm_x6q_kernel<TN, false>, smem);
     hipLaunchKernelGGL((gemm_x6q_kernel<TN, false>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
-                       ldy, rows, ncols, K, C, ntm, ntn, X6Feat{});
+                       ldy, rows, ncols, K, C, ntm, ntn);
   }
 }
 
@@ -1479,7 +1425,7 @@ bool gemm_x6_supported(int K) { return K % X6_BK == 0; }
 
 void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
                             const float* R, int ldr, float* Y, int ldy, int rows, int ncols, int K, int C,
-                            hipStream_t s, X6Feat feat) {
+                            hipStream_t s) {
   switch (v) {
     case 1:
       launch_x6_t<4, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
@@ -1578,13 +1524,13 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
       break;
     // persistent lean
     case 50:
-      launch_x6q_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s, feat);
+      launch_x6q_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
     case 51:
-      launch_x6q_t<6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s, feat);
+      launch_x6q_t<6>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
     case 52:
-      launch_x6q_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s, feat);
+      launch_x6q_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
     // ablations of variant 40 (wrong results; tools/gemm_bench.py only)
     case 91:
@@ -1604,10 +1550,8 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
   }
 }
 
-bool gemm_x6_takes_features(int rows) { return rows >= 65536; }  // the persistent x6q kernels below
-
 void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
-                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s, X6Feat feat) {
+                    float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   // measured on MI355X (tools/gemm_bench.py, K = 256): channel rows take the persistent lean
   // kernel with 256 x 256 tiles (256 x 192 when ncols is a multiple of 192 only); short
   // (log-psi) row counts take 256 x 128 tiles, two workgroups per CU (128 x 192 when ncols
@@ -1618,7 +1562,7 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
     v = (ncols % 192 == 0 && ncols % 256 != 0) ? 51 : 50;
   else
     v = (ncols % 192 == 0) ? 44 : 46;
-  launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s, feat);
+  launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
 }
 
 
