@@ -8,9 +8,13 @@ all-reduce (loss.py:66-92).  Workload: BASELINE.json configs[1] — nspins=[6,0]
 flux=15, default Psiformer (4 heads x 64, 2 layers, 1 determinant), 4096
 walkers per GPU, random-init weights, walkers from init_guess + burn-in.
 
-value = local energies per second over all GPUs (= walkers x GPUs / step time);
-walker_steps_per_sec = 10 x that.  Multi-GPU: weak scaling, walkers sharded,
-one all-reduce of 12 floats per step.
+value = local energies per second over all GPUs (= walkers x GPUs / step time), each
+timed step ending in the host sync of the reference loop (the width adaptation reads
+pmove, mcmc.py:180).  walker_steps_per_sec = B x steps / t(mcmc_step call) from a
+separate region of >= 20 mcmc_step calls (each with its pmove all-reduce and host sync,
+SURVEY.md §8d).  Multi-GPU: weak scaling, walkers sharded, one all-reduce of 16 floats
+per step.  ``--gpus N`` without a torchrun environment starts N rank processes itself
+(one GPU each, RCCL) before anything touches the GPU; rank 0 prints the line.
 """
 
 from __future__ import annotations
@@ -28,7 +32,7 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-METRIC = "local-energies/sec + MCMC walker-steps/sec, N=6 2Q=15, 1/2/4/8 GPUs"
+METRIC = "local-energies/sec + MCMC walker-steps/sec, N={N} 2Q={flux}, 1/2/4/8 GPUs"  # BASELINE.json metric
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_F32_MFMA_TFLOPS  # same guide: f32 MFMA = 1/16 of BF16 (~2.5 PF dense)
 PEAK_HBM_GBS = 8000.0
@@ -53,12 +57,41 @@ def parse():
                     help="walker groups run on parallel HIP streams within one VMC iteration")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="do not record per-kernel HIP events in the timed region (no roofline)")
+    ap.add_argument("--mcmc-calls", type=int, default=20, help="timed mcmc_step calls for walker_steps_per_sec")
+    ap.add_argument("--cpu-c1-seconds", type=float, default=6.0,
+                    help="CPU-baseline budget for BASELINE.json configs[0] (N=3 2Q=2, B=100)")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """torchrun-style launch of n rank processes of this script (one GPU each).  The parent
+    makes no GPU call; rank 0's stdout (the JSON line) is passed through."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].stdout.read().decode()
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
@@ -73,7 +106,7 @@ def main():
     from deephall_amd import _lib, config
     from deephall_amd.hamiltonian import _run_local_energy
     from deephall_amd.loss import device_stats, reduce_stats
-    from deephall_amd.mcmc import make_mcmc_step
+    from deephall_amd.mcmc import make_mcmc_step, update_mcmc_width
     from deephall_amd.networks import make_network
     from deephall_amd.networks.psiformer import get_handle
     from deephall_amd.random import Key, PRNGKey
@@ -94,10 +127,20 @@ def main():
     iteration = make_vmc_iteration(model, B, steps, args.groups)
     iteration1 = make_vmc_iteration(model, B, steps, 1)  # instrumented region: one stream
 
+    import numpy as np
+
+    pmoves = np.zeros(100)
+    t_iter = [0]
+
     def vmc_step(data, key, it=iteration):
+        nonlocal width, pmoves
         data, e_l, obs, n_accept = it(params, data, key, width)
         local_stats = device_stats(model, e_l, obs, n_accept, steps)
         stats = reduce_stats(local_stats)  # the one all-reduce of the step
+        # host side of the reference loop: width adaptation reads pmove (a device sync,
+        # mcmc.py:180 / train.py:131-137)
+        width, pmoves = update_mcmc_width(t_iter[0], width, 100, stats["pmove"], pmoves)
+        t_iter[0] += 1
         return data, stats
 
     for _ in range(args.burn_in):
@@ -149,16 +192,22 @@ def main():
         lib.dh_profile_read(h.h, prof, 1)
         lib.dh_profile_enable(h.h, 0)
 
-    # ---------------- component rates (untimed for `value`): MCMC-only and E_L-only
+    # ---------------- MCMC walker-steps/s: >= 20 mcmc_step calls, each with
+    # its pmove all-reduce and the host read of pmove; then the E_L-only rate
     t_mcmc = t_el = float("nan")
     if not args.no_components:
         barrier()
         a = time.perf_counter()
-        for _ in range(3):
-            data, _ = mcmc_step(params, data, key, width, reduce=False)
+        for _ in range(args.mcmc_calls):
+            data, pm = mcmc_step(params, data, key, width)
+            float(pm)  # device sync, as pmove.item() in update_mcmc_width
             key = key.advance(steps)
         barrier()
-        t_mcmc = (time.perf_counter() - a) / 3
+        t_mcmc = time.perf_counter() - a
+        tm = torch.tensor([t_mcmc], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        t_mcmc = float(tm.item()) / args.mcmc_calls
         a = time.perf_counter()
         for _ in range(3):
             _run_local_energy(model, params, data)
@@ -232,8 +281,9 @@ def main():
     B_total = B * world
     value = B_total * args.steps / dt
     F_fwd = 2 * N * 4 * 256 + 2 * (12 * N * 256**2 + 4 * N * N * 256) + 4 * N * 256 * (args.flux + 1) * N
+    metric = METRIC.format(N=N, flux=args.flux)
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 1),
         "unit": "local-energies/s",
         "n_gpus": world,
@@ -254,11 +304,12 @@ def main():
             "walker_groups_per_gpu": args.groups,
             "gemm_arithmetic": gemm_mode,
         },
-        "walker_steps_per_sec": round(value * steps, 1),
+        "walker_steps_per_sec": round(B_total * steps / t_mcmc, 1) if t_mcmc == t_mcmc else None,
+        "walker_steps_per_sec_def": (f"B_total x steps / t(mcmc_step call), mean of {args.mcmc_calls} calls incl. "
+                                     "the initial log-psi pass, the pmove all-reduce and the host sync"),
         "components": {
             "mcmc_step_ms": round(1e3 * t_mcmc, 3),
             "local_energy_ms": round(1e3 * t_el, 3),
-            "walker_steps_per_sec_mcmc_only": round(B_total * steps / t_mcmc, 1),
             "local_energies_per_sec_el_only": round(B_total / t_el, 1),
             "model_tflops_el_only": round(B_total * (2 * N + 5) * F_fwd / t_el / 1e12, 2),
             "model_tflops_mcmc_only": round(B_total * (steps + 1) * F_fwd / t_mcmc / 1e12, 2),
@@ -273,19 +324,29 @@ def main():
         from oracle import cpu_baseline
         from oracle.reference import OracleConfig
 
+        # the GPU box gives one GPU's job a 16-CPU share (os.cpu_count() reports the whole host)
         threads = min(16, os.cpu_count() or 1)
         cb = cpu_baseline.measure(
             OracleConfig(nspins=tuple(args.nspins), flux=args.flux), steps=steps,
             budget_s=args.cpu_baseline_seconds, threads=threads,
         )
+        c1 = cpu_baseline.measure(OracleConfig(nspins=(3, 0), flux=2), steps=steps, budget_s=args.cpu_c1_seconds,
+                                  threads=threads, el_batch=20, fwd_batch=100)
         out["cpu_baseline"] = {
             "value": round(cb["local_energies_per_sec"], 3),
             "unit": "local-energies/s",
             "cores": cb["threads"],
             "kind": "port",
             "sample": cb["sample"],
+            "cpu_model": cb["cpu_model"],
+            "host_cpus": cb["host_cpus"],
+            "cores_note": "16 threads = the CPU share gpurun gives a one-GPU job (the host has more cores)",
             "walker_steps_per_sec": round(cb["walker_steps_per_sec"] * steps / (steps + 1), 1),
             "el_only_per_sec": round(cb["el_only_per_sec"], 3),
+            "c1": {"config": "nspins=[3,0] flux=2 (BASELINE.json configs[0]), vmap batches of the B=100 walkers",
+                   "local_energies_per_sec": round(c1["local_energies_per_sec"], 3),
+                   "walker_steps_per_sec": round(c1["walker_steps_per_sec"] * steps / (steps + 1), 1),
+                   "sample": c1["sample"]},
         }
     print(json.dumps(out))
     if world > 1:

@@ -26,6 +26,9 @@ STAT_NAMES = [
     "angular_momentum_square",
     "pmove",
     "nvalid",
+    "clipped_lz2",
+    "clipped_lz",
+    "clipped_l2",
 ]
 
 EXPORTS = [
@@ -41,6 +44,7 @@ EXPORTS = [
     "dh_mcmc_step",
     "dh_local_energy",
     "dh_energy_stats",
+    "dh_loss_diff",
     "dh_init_walkers",
     "dh_potential",
     "dh_debug_trunk",
@@ -50,6 +54,12 @@ EXPORTS = [
     "dh_debug_x6_plane_rows",
     "dh_debug_split_planes",
     "dh_debug_gemm_x6",
+    "dh_ref_layout",
+    "dh_set_params_ref",
+    "dh_vjp_workspace_bytes",
+    "dh_logpsi_vjp",
+    "dh_grad_cotangent",
+    "dh_adam_update",
     "dh_profile_enable",
     "dh_profile_read",
     "dh_debug_f_offset",
@@ -112,8 +122,11 @@ def load(path: Path | str | None = None):
     lib.dh_mcmc_step.restype = i32
     lib.dh_local_energy.argtypes = [vp, vp, i32, vp, vp, vp, sz, vp]
     lib.dh_local_energy.restype = i32
-    lib.dh_energy_stats.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, sz, vp]
+    lib.dh_energy_stats.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp]
     lib.dh_energy_stats.restype = i32
+    f32 = C.c_float
+    lib.dh_loss_diff.argtypes = [vp, vp, vp, i32, vp, f32, f32, f32, vp, vp, vp]
+    lib.dh_loss_diff.restype = i32
     lib.dh_init_walkers.argtypes = [vp, vp, i32, u64, i64, vp]
     lib.dh_init_walkers.restype = i32
     lib.dh_potential.argtypes = [vp, vp, i32, vp, vp]
@@ -134,6 +147,18 @@ def load(path: Path | str | None = None):
     lib.dh_debug_split_planes.restype = i32
     lib.dh_debug_gemm_x6.argtypes = [i32, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp]
     lib.dh_debug_gemm_x6.restype = i32
+    lib.dh_ref_layout.argtypes = [vp, C.POINTER(sz), i32]
+    lib.dh_ref_layout.restype = i32
+    lib.dh_set_params_ref.argtypes = [vp, vp, sz, vp]
+    lib.dh_set_params_ref.restype = i32
+    lib.dh_vjp_workspace_bytes.argtypes = [vp, i32]
+    lib.dh_vjp_workspace_bytes.restype = sz
+    lib.dh_logpsi_vjp.argtypes = [vp, vp, i32, vp, vp, vp, vp, sz, vp]
+    lib.dh_logpsi_vjp.restype = i32
+    lib.dh_grad_cotangent.argtypes = [vp, vp, i32, i32, vp, vp]
+    lib.dh_grad_cotangent.restype = i32
+    lib.dh_adam_update.argtypes = [vp, vp, vp, vp, sz, f32, f32, f32, f32, i32, vp]
+    lib.dh_adam_update.restype = i32
     lib.dh_profile_enable.argtypes = [vp, i32]
     lib.dh_profile_enable.restype = i32
     lib.dh_profile_read.argtypes = [vp, C.POINTER(C.c_double), i32]

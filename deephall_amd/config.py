@@ -1,7 +1,8 @@
 """Configuration dataclasses — the fields of deephall/config.py:56-214 the hot path reads.
 
 Field names, defaults and meaning follow the reference exactly (System 56-79,
-PsiformerNetwork 92-97, Network 100-104, MCMC 107-122, Config 201-214).  The
+PsiformerNetwork 92-97, Network 100-104, MCMC 107-122, LearningRate / optimizers
+125-165, Log 168-198, Config 201-214).  The
 OmegaConf machinery is out of scope; ``Config.from_dict`` mirrors the reference's
 ``from_dict`` (config.py:23-48: nested dataclasses, extra keys ignored).
 The reference needs Python >= 3.11 (``StrEnum``); these are ``str`` Enums.
@@ -84,9 +85,53 @@ class MCMC:
 
 
 @dataclass
+class LearningRate:
+    """rate * (1 / (1 + t / delay)) ** decay (config.py:125-137)."""
+
+    rate: float = 0.005
+    decay: float = 1.0
+    delay: float = 2000.0
+
+    def schedule(self, t):
+        return self.rate * (1.0 / (1.0 + (t / self.delay))) ** self.decay
+
+
+class OptimizerName(str, enum.Enum):
+    adam = "adam"
+    kfac = "kfac"
+    none = "none"
+
+
+@dataclass
+class OptimizerAdam:
+    lr: LearningRate = field(default_factory=LearningRate)
+
+
+@dataclass
+class OptimizerKfac:
+    lr: LearningRate = field(default_factory=lambda: LearningRate(rate=0.05))
+
+
+@dataclass
 class Optim:
+    """config.py:160-165.  The reference's default optimizer is KFAC, which is not built
+    on MI355X (optimizers.py raises for it); Adam and 'none' are."""
+
     iterations: int = 1000
-    optimizer: Optional[str] = "none"  # only the inference ("none") step is in scope
+    optimizer: Optional[OptimizerName] = OptimizerName.kfac
+    adam: OptimizerAdam = field(default_factory=OptimizerAdam)
+    kfac: OptimizerKfac = field(default_factory=OptimizerKfac)
+
+
+@dataclass
+class Log:
+    """config.py:168-198."""
+
+    save_path: Optional[str] = None
+    restore_path: Optional[str] = None
+    save_time_interval: int = 10 * 60
+    save_step_interval: int = 1000
+    initial_energy: bool = True
 
 
 @dataclass
@@ -97,6 +142,7 @@ class Config:
     network: Network = field(default_factory=Network)
     mcmc: MCMC = field(default_factory=MCMC)
     optim: Optim = field(default_factory=Optim)
+    log: Log = field(default_factory=Log)
 
     @classmethod
     def from_dict(cls, dikt: dict[str, Any]) -> "Config":

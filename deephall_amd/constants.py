@@ -34,6 +34,15 @@ def pmean(x: torch.Tensor) -> torch.Tensor:
     return y / n
 
 
+def pmean_(x: torch.Tensor) -> torch.Tensor:
+    """In-place mean over ranks (one all-reduce; identity on one process)."""
+    n = world_size()
+    if n > 1:
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        x.div_(n)
+    return x
+
+
 def pmap(func, *args, **kwargs):
     """The per-device function already runs on this rank's shard: identity wrapper."""
     return func

@@ -93,14 +93,19 @@ struct dh_handle {
   dh_config cfg;
   Dims d;
   Params p{};
-  std::vector<size_t> offsets;  // nseg + 1
+  std::vector<size_t> offsets;      // packed layout, nseg + 1
+  std::vector<size_t> ref_offsets;  // reference-tree layout (dh_ref_layout), nseg + 1
   float* params = nullptr;
+  float* ref = nullptr;      // reference-layout copy (dh_set_params_ref; needed by the VJP)
+  uint16_t* wb = nullptr;    // backward split-bf16 planes (untransposed weights)
+  float* wbt = nullptr;      // backward exact-f32 transposed weights (D % 32 != 0)
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
   float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
   uint16_t* wp = nullptr;  // split-bf16 weight planes for the x6 kernels (device)
   int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
   bool params_set = false;
+  bool ref_set = false;
   Profiler prof;
 };
 
@@ -195,6 +200,28 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
     off += align64(s);
   }
   h->offsets.push_back(off);
+  // reference parameter tree, flattened in SURVEY.md Appendix B order (ref_seg below)
+  {
+    const size_t DD = (size_t)D * D, MNK = (size_t)d.M * N * d.K;
+    std::vector<size_t> rs;
+    rs.push_back((size_t)4 * D);
+    for (int l = 0; l < d.L; ++l)
+      for (size_t v : {DD, (size_t)D, DD, (size_t)D, DD, (size_t)D, DD, (size_t)D, DD, (size_t)D, (size_t)D, DD,
+                       (size_t)D, (size_t)D, (size_t)D})
+        rs.push_back(v);
+    for (int i = 0; i < 2 * d.NB; ++i) {
+      rs.push_back((size_t)D * MNK);
+      rs.push_back(MNK);
+    }
+    rs.push_back(1);
+    rs.push_back(1);
+    size_t ro = 0;
+    for (size_t v : rs) {
+      h->ref_offsets.push_back(ro);
+      ro += align64(v);
+    }
+    h->ref_offsets.push_back(ro);
+  }
   // monopole-harmonic normalisation sqrt(C(2Q, Q-m)) (blocks.py:45-46), index p = Q+m
   std::vector<float> norm(d.M);
   for (int p = 0; p < d.M; ++p) {
@@ -217,6 +244,9 @@ void dh_destroy(dh_handle* h) {
   if (h->norm) (void)hipFree(h->norm);
   if (h->wt) (void)hipFree(h->wt);
   if (h->wp) (void)hipFree(h->wp);
+  if (h->ref) (void)hipFree(h->ref);
+  if (h->wb) (void)hipFree(h->wb);
+  if (h->wbt) (void)hipFree(h->wbt);
   delete h;
 }
 
@@ -227,15 +257,23 @@ int dh_param_layout(const dh_handle* h, size_t* offsets, int n) {
   return nseg;
 }
 
-int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream) {
-  if (!h || !params) return fail(DH_EINVAL, "null argument");
-  if (count != h->offsets.back()) return fail(DH_EINVAL, "parameter count mismatch");
-  if (!h->params) HIP_TRY(hipMalloc(&h->params, count * sizeof(float)));
-  if (!h->norm) {
-    HIP_TRY(hipMalloc(&h->norm, h->norm_host.size() * sizeof(float)));
-    HIP_TRY(hipMemcpy(h->norm, h->norm_host.data(), h->norm_host.size() * sizeof(float), hipMemcpyHostToDevice));
-  }
-  HIP_TRY(hipMemcpyAsync(h->params, params, count * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}  // extern "C"
+
+namespace {
+
+// Reference-tree segment indices (dh_ref_layout)
+struct RefSeg {
+  int L, NB;
+  int W0() const { return 0; }
+  int lay(int l, int k) const { return 1 + 15 * l + k; }  // k: Wq bq Wk bk Wv bv Wo bo Wl ln1s ln1b Wm bm ln2s ln2b
+  int orb_kernel(int i) const { return 1 + 15 * L + 2 * i; }
+  int orb_bias(int i) const { return 2 + 15 * L + 2 * i; }
+  int jas(int k) const { return 1 + 15 * L + 4 * NB + k; }
+};
+enum { RWq = 0, Rbq, RWk, Rbk, RWv, Rbv, RWo, Rbo, RWl, Rln1s, Rln1b, RWm, Rbm, Rln2s, Rln2b };
+
+// Device pointers of the packed segments.
+void assign_packed(dh_handle* h) {
   const Dims& d = h->d;
   const float* P = h->params;
   int s = 0;
@@ -255,15 +293,20 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
   h->p.borb = P + h->offsets[s++];
   h->p.jastrow = P + h->offsets[s++];
   h->p.W0qkv = P + h->offsets[s++];
-  // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
-  // NT GEMM kernels whose LDS-DMA staging wants k contiguous in both operands.
+}
+
+// Derived weight copies: transposed + split-bf16 planes for the forward NT/x6 GEMMs, and the
+// backward copies (planes of the untransposed weights, or W^T when D % 32 != 0).
+int derive_weights(dh_handle* h, hipStream_t st) {
+  const Dims& d = h->d;
+  const int D = d.D;
   if (d.D % 32 == 0) {
-    const int D = d.D;
+    // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
+    // NT GEMM kernels whose LDS-DMA staging wants k contiguous in both operands.
     const size_t sq = (size_t)round_up(D, kRowPad) * D, sqkv = (size_t)round_up(3 * D, kRowPad) * D;
     const size_t sorb = (size_t)round_up(d.orb_cols, kRowPad) * D;
     const size_t total = (size_t)d.L * (sqkv + 2 * sq) + sorb;
     if (!h->wt) HIP_TRY(hipMalloc(&h->wt, total * sizeof(float)));
-    hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(h->wt, 0, total * sizeof(float), st));
     float* q = h->wt;
     for (int l = 0; l < d.L; ++l) {
@@ -300,9 +343,133 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
     }
     launch_split_planes(h->p.WorbT, D, d.orb_cols, D, w, st);
     h->p.WorbP = w;
-    HIP_TRY(hipGetLastError());
+    // backward planes: the untransposed W [K = D][n] read as a transposed weight with D
+    // output rows and contraction length n (dX = dY W^T)
+    const int pr = x6_plane_rows(D);
+    const size_t bq = (size_t)3 * pr * 3 * D, bd = (size_t)3 * pr * D, bo = (size_t)3 * pr * d.ld_orb;
+    const size_t btotal = (size_t)d.L * (bq + 2 * bd) + bo;
+    if (!h->wb) HIP_TRY(hipMalloc(&h->wb, btotal * sizeof(uint16_t)));
+    uint16_t* b = h->wb;
+    for (int l = 0; l < d.L; ++l) {
+      LayerParams& lp = h->p.layer[l];
+      launch_split_planes(lp.Wqkv, 3 * D, D, 3 * D, b, st);
+      lp.WqkvB = b;
+      b += bq;
+      launch_split_planes(lp.Wol, D, D, D, b, st);
+      lp.WolB = b;
+      b += bd;
+      launch_split_planes(lp.Wm, D, D, D, b, st);
+      lp.WmB = b;
+      b += bd;
+    }
+    launch_split_planes(h->p.Worb, d.ld_orb, D, d.ld_orb, b, st);
+    h->p.WorbB = b;
+  } else {
+    // exact-f32 backward: W^T [n][D]
+    const size_t total = (size_t)d.L * (5 * (size_t)D * D) + (size_t)d.ld_orb * D;
+    if (!h->wbt) HIP_TRY(hipMalloc(&h->wbt, total * sizeof(float)));
+    HIP_TRY(hipMemsetAsync(h->wbt, 0, total * sizeof(float), st));
+    float* q = h->wbt;
+    for (int l = 0; l < d.L; ++l) {
+      LayerParams& lp = h->p.layer[l];
+      launch_transpose(lp.Wqkv, 3 * D, D, 3 * D, q, D, st);
+      lp.WqkvBT = q;
+      q += (size_t)3 * D * D;
+      launch_transpose(lp.Wol, D, D, D, q, D, st);
+      lp.WolBT = q;
+      q += (size_t)D * D;
+      launch_transpose(lp.Wm, D, D, D, q, D, st);
+      lp.WmBT = q;
+      q += (size_t)D * D;
+    }
+    launch_transpose(h->p.Worb, d.ld_orb, D, d.orb_cols, q, D, st);
+    h->p.WorbBT = q;
   }
+  HIP_TRY(hipGetLastError());
+  return DH_OK;
+}
+
+int ensure_param_buffers(dh_handle* h) {
+  if (!h->params) HIP_TRY(hipMalloc(&h->params, h->offsets.back() * sizeof(float)));
+  if (!h->norm) {
+    HIP_TRY(hipMalloc(&h->norm, h->norm_host.size() * sizeof(float)));
+    HIP_TRY(hipMemcpy(h->norm, h->norm_host.data(), h->norm_host.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
+  return DH_OK;
+}
+
+// Pack the reference tree (h->ref) into the kernel layout: concatenations, zero padding and
+// the three folds (Wo Wl, bo Wl, W0 Wqkv) as double-accumulated products.
+void pack_from_ref(dh_handle* h, hipStream_t st) {
+  const Dims& d = h->d;
+  const int D = d.D, MNK = d.M * d.N * d.K;
+  const RefSeg R{d.L, d.NB};
+  auto ref = [&](int seg) { return h->ref + h->ref_offsets[seg]; };
+  auto pk = [&](int seg) { return h->params + h->offsets[seg]; };
+  launch_copy2d(ref(R.W0()), D, pk(0), D, 4, D, st);
+  for (int l = 0; l < d.L; ++l) {
+    const int b = 1 + 8 * l;
+    for (int part = 0; part < 3; ++part) {
+      launch_copy2d(ref(R.lay(l, RWq + 2 * part)), D, pk(b + 0) + part * D, 3 * D, D, D, st);
+      launch_copy2d(ref(R.lay(l, Rbq + 2 * part)), D, pk(b + 1) + part * D, 3 * D, 1, D, st);
+    }
+    launch_small_gemm(D, D, D, ref(R.lay(l, RWo)), D, 0, ref(R.lay(l, RWl)), D, 0, pk(b + 2), D, 0, st);
+    launch_small_gemm(1, D, D, ref(R.lay(l, Rbo)), D, 0, ref(R.lay(l, RWl)), D, 0, pk(b + 3), D, 0, st);
+    launch_copy2d(ref(R.lay(l, Rln1s)), D, pk(b + 4), D, 1, D, st);
+    launch_copy2d(ref(R.lay(l, Rln1b)), D, pk(b + 4) + D, D, 1, D, st);
+    launch_copy2d(ref(R.lay(l, RWm)), D, pk(b + 5), D, D, D, st);
+    launch_copy2d(ref(R.lay(l, Rbm)), D, pk(b + 6), D, 1, D, st);
+    launch_copy2d(ref(R.lay(l, Rln2s)), D, pk(b + 7), D, 1, D, st);
+    launch_copy2d(ref(R.lay(l, Rln2b)), D, pk(b + 7) + D, D, 1, D, st);
+  }
+  const int so = 1 + 8 * d.L;
+  launch_copy2d(nullptr, 0, pk(so), d.ld_orb, D, d.ld_orb, st);
+  launch_copy2d(nullptr, 0, pk(so + 1), d.ld_orb, 1, d.ld_orb, st);
+  for (int i = 0; i < 2 * d.NB; ++i) {
+    launch_copy2d(ref(R.orb_kernel(i)), MNK, pk(so) + i * MNK, d.ld_orb, D, MNK, st);
+    launch_copy2d(ref(R.orb_bias(i)), MNK, pk(so + 1) + i * MNK, d.ld_orb, 1, MNK, st);
+  }
+  launch_copy2d(ref(R.jas(0)), 1, pk(so + 2), 1, 1, 1, st);
+  launch_copy2d(ref(R.jas(1)), 1, pk(so + 2) + 1, 1, 1, 1, st);
+  if (d.L > 0) launch_small_gemm(4, 3 * D, D, pk(0), D, 0, pk(1), 3 * D, 0, pk(so + 3), 3 * D, 0, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream) {
+  if (!h || !params) return fail(DH_EINVAL, "null argument");
+  if (count != h->offsets.back()) return fail(DH_EINVAL, "parameter count mismatch");
+  if (int rc = ensure_param_buffers(h)) return rc;
+  HIP_TRY(hipMemcpyAsync(h->params, params, count * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  assign_packed(h);
+  if (int rc = derive_weights(h, (hipStream_t)stream)) return rc;
   h->params_set = true;
+  h->ref_set = false;  // a packed upload has no reference tree (the VJP needs one)
+  return DH_OK;
+}
+
+int dh_ref_layout(const dh_handle* h, size_t* offsets, int n) {
+  if (!h) return fail(DH_EINVAL, "null handle");
+  const int nseg = (int)h->ref_offsets.size() - 1;
+  for (int i = 0; i < n && i <= nseg; ++i) offsets[i] = h->ref_offsets[i];
+  return nseg;
+}
+
+int dh_set_params_ref(dh_handle* h, const float* ref, size_t count, void* stream) {
+  if (!h || !ref) return fail(DH_EINVAL, "null argument");
+  if (count != h->ref_offsets.back()) return fail(DH_EINVAL, "reference parameter count mismatch");
+  if (int rc = ensure_param_buffers(h)) return rc;
+  if (!h->ref) HIP_TRY(hipMalloc(&h->ref, count * sizeof(float)));
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h->ref, ref, count * sizeof(float), hipMemcpyDeviceToDevice, st));
+  pack_from_ref(h, st);
+  HIP_TRY(hipGetLastError());
+  assign_packed(h);
+  if (int rc = derive_weights(h, st)) return rc;
+  h->params_set = true;
+  h->ref_set = true;
   return DH_OK;
 }
 
@@ -491,13 +658,229 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
   return DH_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Workspace of one gradient (VJP) pass over nw walkers (floats).
+struct GradWork {
+  float *geo, *logpsi, *F, *dF, *jg;
+  float *hs[17], *qkv[16], *o[16], *t[16], *h1[16], *z[16];  // saved activations per layer
+  float *dh, *dA, *dz, *dqkv, *dO;                            // backward temporaries
+  float *P, *dWol, *dbol;                                     // chunk partials, folded-weight grads
+  size_t total_bytes;
+};
+
+GradWork carve_grad(const Dims& d, int nw, void* base) {
+  const int rows = nw * d.N;
+  const size_t rp = (size_t)round_up(std::max(rows, 1), kRowPad);
+  const size_t D = d.D, nh = align64(rp * D);
+  GradWork w{};
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    float* p = base ? reinterpret_cast<float*>(base) + off : nullptr;
+    off += align64(n);
+    return p;
+  };
+  w.geo = take((size_t)rows * 4);
+  w.logpsi = take((size_t)nw * 2);
+  w.jg = take((size_t)nw * 2);
+  w.F = take(rp * d.ld_orb);
+  w.dF = take(rp * d.ld_orb);
+  for (int l = 0; l <= d.L; ++l) w.hs[l] = take(nh);
+  for (int l = 0; l < d.L; ++l) {
+    w.qkv[l] = take(3 * nh);
+    w.o[l] = take(nh);
+    w.t[l] = take(nh);
+    w.h1[l] = take(nh);
+    w.z[l] = take(nh);
+  }
+  w.dh = take(nh);
+  w.dA = take(nh);
+  w.dz = take(nh);
+  w.dqkv = take(3 * nh);
+  w.dO = take(nh);
+  const size_t nch = (size_t)grad_chunks(rows);
+  const size_t pw = std::max({D * 3 * D, D * (size_t)d.ld_orb, (size_t)4 * D});
+  const size_t pc = std::max((size_t)3 * D, (size_t)d.ld_orb);
+  w.P = take(std::max({nch * pw, nch * pc, (size_t)ln_bwd_blocks(rows) * 2 * D, (size_t)nw * 2}));
+  w.dWol = take(D * D);
+  w.dbol = take(D);
+  w.total_bytes = off * sizeof(float);
+  return w;
+}
+
+// One chunk of the VJP: forward with saved activations, then the chain rule back to every
+// reference parameter; gradient written (acc = 0) or accumulated (acc = 1) into `grad`
+// (dh_ref_layout).  ct: per-walker cotangents [nw][2].
+int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, float* logpsi, int acc,
+            const GradWork& w, hipStream_t s) {
+  const Dims& d = h->d;
+  const Params& P = h->p;
+  const int rows = nw * d.N, D = d.D, nch = grad_chunks(rows);
+  const bool x6 = d.D % 32 == 0 && gemm_x6_supported(D);
+  const RefSeg RS{d.L, d.NB};
+  auto g = [&](int seg) { return grad + h->ref_offsets[seg]; };
+  auto ref = [&](int seg) { return (const float*)h->ref + h->ref_offsets[seg]; };
+  // forward GEMM Y = X W (+ bias) (+ R): the same arithmetic as the log-psi pass
+  auto fwd = [&](const float* X, const float* W, const float* Wt, const uint16_t* Wp, int ncols, const float* bias,
+                 const float* Rr, float* Y) {
+    if (x6)
+      launch_gemm_x6(X, D, Wp, x6_plane_rows(ncols), bias, Rr, ncols, Y, ncols, rows, ncols, D, 1, s);
+    else if (Wt)
+      launch_gemm_nt(X, D, Wt, D, bias, Rr, ncols, Y, ncols, rows, ncols, D, 1, s);
+    else
+      launch_gemm(X, D, W, ncols, bias, Rr, ncols, Y, ncols, rows, ncols, D, 1, s);
+  };
+  // backward GEMM dX = dY W^T (+ R) with W [D][n]
+  auto bwd = [&](const float* dY, int n, const uint16_t* WB, const float* WBT, const float* Rr, float* dX) {
+    if (x6)
+      launch_gemm_x6(dY, n, WB, x6_plane_rows(D), nullptr, Rr, D, dX, D, rows, D, n, 1, s);
+    else
+      launch_gemm(dY, n, WBT, D, nullptr, Rr, D, dX, D, rows, D, n, 1, s);
+  };
+  // weight gradient: out[:, c0:c0+nc] (ldo) (+)= X^T dY[:, c0:c0+nc] over this chunk's rows
+  auto wgrad = [&](const float* X, const float* dY, int n) { launch_tn_partial(X, D, dY, n, rows, D, n, w.P, s); };
+  auto wout = [&](int n, int c0, int nc, float* out, int ldo) {
+    launch_reduce2d(w.P + c0, nch, (size_t)D * n, n, D, nc, out, ldo, 1.f, acc, s);
+  };
+  auto bgrad = [&](const float* dY, int n, int c0, int nc, float* out) {
+    launch_colsum_partial(dY, n, rows, n, w.P, s);
+    launch_reduce2d(w.P + c0, nch, (size_t)n, n, 1, nc, out, nc, 1.f, acc, s);
+  };
+  // ---- forward with saved activations
+  launch_input(d, x, P.W0, nullptr, nullptr, w.hs[0], nullptr, w.geo, nw, 1, s);
+  for (int l = 0; l < d.L; ++l) {
+    const LayerParams& lp = P.layer[l];
+    fwd(w.hs[l], lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, w.qkv[l]);
+    launch_attention(d, w.qkv[l], w.geo, w.o[l], nw, 1, s);
+    fwd(w.o[l], lp.Wol, lp.WolT, lp.WolP, D, lp.bol, w.hs[l], w.t[l]);
+    launch_ln_fwd(w.t[l], nullptr, lp.ln1, w.h1[l], rows, D, s);
+    fwd(w.h1[l], lp.Wm, lp.WmT, lp.WmP, D, lp.bm, nullptr, w.z[l]);
+    launch_ln_fwd(w.h1[l], w.z[l], lp.ln2, w.hs[l + 1], rows, D, s);
+  }
+  {
+    const float* hL = w.hs[d.L];
+    if (x6)
+      launch_gemm_x6(hL, D, P.WorbP, x6_plane_rows(d.orb_cols), P.borb, nullptr, 0, w.F, d.ld_orb, rows, d.orb_cols,
+                     D, 1, s);
+    else if (P.WorbT)
+      launch_gemm_nt(hL, D, P.WorbT, D, P.borb, nullptr, 0, w.F, d.ld_orb, rows, d.orb_cols, D, 1, s);
+    else
+      launch_gemm(hL, D, P.Worb, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, rows, d.orb_cols, D, 1, s);
+  }
+  launch_det_value(d, w.F, x, P.jastrow, h->norm, logpsi ? logpsi : w.logpsi, nw, s);
+  // ---- backward
+  launch_det_bwd(d, w.F, x, P.jastrow, h->norm, ct, w.dF, w.jg, nw, s);
+  launch_reduce2d(w.jg, nw, 2, 2, 1, 1, g(RS.jas(0)), 1, 1.f, acc, s);
+  launch_reduce2d(w.jg + 1, nw, 2, 2, 1, 1, g(RS.jas(1)), 1, 1.f, acc, s);
+  {
+    const int MNK = d.M * d.N * d.K;
+    wgrad(w.hs[d.L], w.dF, d.ld_orb);
+    for (int i = 0; i < 2 * d.NB; ++i) wout(d.ld_orb, i * MNK, MNK, g(RS.orb_kernel(i)), MNK);
+    launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
+    for (int i = 0; i < 2 * d.NB; ++i)
+      launch_reduce2d(w.P + i * MNK, nch, (size_t)d.ld_orb, d.ld_orb, 1, MNK, g(RS.orb_bias(i)), MNK, 1.f, acc, s);
+    bwd(w.dF, d.ld_orb, P.WorbB, P.WorbBT, nullptr, w.dh);
+  }
+  for (int l = d.L - 1; l >= 0; --l) {
+    const LayerParams& lp = P.layer[l];
+    const int nb = ln_bwd_blocks(rows);
+    // h_{l+1} = LN2(h1 + tanh z): dU -> dA (the residual path into h1), dz
+    launch_ln_bwd(w.h1[l], w.z[l], lp.ln2, w.dh, nullptr, w.dA, w.dz, w.P, rows, D, s);
+    launch_reduce2d(w.P, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln2s)), D, 1.f, acc, s);
+    launch_reduce2d(w.P + D, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln2b)), D, 1.f, acc, s);
+    // z = h1 Wm + bm
+    wgrad(w.h1[l], w.dz, D);
+    wout(D, 0, D, g(RS.lay(l, RWm)), D);
+    bgrad(w.dz, D, 0, D, g(RS.lay(l, Rbm)));
+    bwd(w.dz, D, lp.WmB, lp.WmBT, w.dA, w.dh);  // dh1 = dU + dz Wm^T
+    // h1 = LN1(t): dT -> dA
+    launch_ln_bwd(w.t[l], nullptr, lp.ln1, w.dh, nullptr, w.dA, nullptr, w.P, rows, D, s);
+    launch_reduce2d(w.P, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln1s)), D, 1.f, acc, s);
+    launch_reduce2d(w.P + D, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln1b)), D, 1.f, acc, s);
+    // t = h + o Wol + bol: folded-weight gradients, then unfolded onto Wo, bo, Wl
+    wgrad(w.o[l], w.dA, D);
+    launch_reduce2d(w.P, nch, (size_t)D * D, D, D, D, w.dWol, D, 1.f, 0, s);
+    launch_colsum_partial(w.dA, D, rows, D, w.P, s);
+    launch_reduce2d(w.P, nch, (size_t)D, D, 1, D, w.dbol, D, 1.f, 0, s);
+    //   Wol = Wo Wl, bol = bo Wl:  dWo = dWol Wl^T, dbo = dbol Wl^T, dWl = Wo^T dWol + bo^T dbol
+    launch_small_gemm(D, D, D, w.dWol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, RWo)), D, acc, s);
+    launch_small_gemm(1, D, D, w.dbol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, Rbo)), D, acc, s);
+    launch_small_gemm(D, D, D, ref(RS.lay(l, RWo)), D, 1, w.dWol, D, 0, g(RS.lay(l, RWl)), D, acc, s);
+    launch_small_gemm(D, D, 1, ref(RS.lay(l, Rbo)), 1, 0, w.dbol, D, 0, g(RS.lay(l, RWl)), D, 1, s);
+    bwd(w.dA, D, lp.WolB, lp.WolBT, nullptr, w.dO);  // dO = dT Wol^T
+    launch_attn_bwd(d, w.qkv[l], w.dO, w.dqkv, nw, s);
+    // qkv = h Wqkv + bqkv
+    wgrad(w.hs[l], w.dqkv, 3 * D);
+    for (int part = 0; part < 3; ++part) wout(3 * D, part * D, D, g(RS.lay(l, RWq + 2 * part)), D);
+    launch_colsum_partial(w.dqkv, 3 * D, rows, 3 * D, w.P, s);
+    for (int part = 0; part < 3; ++part)
+      launch_reduce2d(w.P + part * D, nch, (size_t)3 * D, 3 * D, 1, D, g(RS.lay(l, Rbq + 2 * part)), D, 1.f, acc,
+                      s);
+    bwd(w.dqkv, 3 * D, lp.WqkvB, lp.WqkvBT, w.dA, w.dh);  // dh_l = dT + dqkv Wqkv^T
+  }
+  // h_0 = features W0
+  launch_w0_partial(d, w.geo, w.dh, D, rows, w.P, s);
+  launch_reduce2d(w.P, nch, (size_t)4 * D, D, 4, D, g(RS.W0()), D, 1.f, acc, s);
+  return check_launch();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dh_vjp_workspace_bytes(const dh_handle* h, int batch) {
+  if (!h || batch < 1) return 0;
+  return carve_grad(h->d, batch, nullptr).total_bytes;
+}
+
+int dh_logpsi_vjp(dh_handle* h, const float* x, int B, const float* ct, float* grad, float* logpsi, void* ws,
+                  size_t ws_bytes, void* stream) {
+  const size_t need1 = h ? dh_vjp_workspace_bytes(h, 1) : 0;
+  if (int rc = check_common(h, x, B, ws, ws_bytes, need1)) return rc;
+  if (!h->ref_set) return fail(DH_ESTATE, "the VJP needs parameters uploaded with dh_set_params_ref");
+  if (!ct || !grad) return fail(DH_EINVAL, "null argument");
+  if (h->d.D > 1024 || h->d.dh > 1024) return fail(DH_EINVAL, "VJP supports D <= 1024");
+  int chunk = B;
+  while (chunk > 1 && dh_vjp_workspace_bytes(h, chunk) > ws_bytes) chunk = (chunk + 1) / 2;
+  hipStream_t s = (hipStream_t)stream;
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nw = std::min(chunk, B - b0);
+    GradWork w = carve_grad(h->d, nw, ws);
+    if (int rc = run_vjp(h, x + (size_t)b0 * h->d.N * 2, nw, ct + 2 * (size_t)b0, grad,
+                         logpsi ? logpsi + 2 * (size_t)b0 : nullptr, b0 > 0, w, s))
+      return rc;
+  }
+  return DH_OK;
+}
+
+int dh_grad_cotangent(const float* diff, const float* nvalid, int B, int part, float* ct, void* stream) {
+  if (!diff || !nvalid || !ct || B < 1 || (part != 0 && part != 1)) return fail(DH_EINVAL, "bad arguments");
+  launch_cotangent(diff, nvalid, B, part, ct, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_adam_update(float* params, const float* grad, float* mu, float* nu, size_t n, float lr, float b1, float b2,
+                   float eps, int step, void* stream) {
+  if (!params || !grad || !mu || !nu || n == 0 || step < 0) return fail(DH_EINVAL, "bad arguments");
+  launch_adam(params, grad, mu, nu, n, lr, b1, b2, eps, step, (hipStream_t)stream);
+  return check_launch();
+}
+
 int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int32_t* n_accept, int B, int steps,
-                    float* out, void* ws, size_t ws_bytes, void* stream) {
-  (void)ws;
-  (void)ws_bytes;
+                    int penalties, float* out, void* stream) {
   if (!h || !e_l || !obs || !out) return fail(DH_EINVAL, "null argument");
-  if (B < 1 || B > 32768) return fail(DH_EINVAL, "dh_energy_stats supports 1 <= B <= 32768");
-  launch_stats(e_l, obs, n_accept, B, steps, out, nullptr, (hipStream_t)stream);
+  if (B < 1) return fail(DH_EINVAL, "dh_energy_stats needs B >= 1");
+  launch_stats(e_l, obs, n_accept, B, steps, penalties, out, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const float* stats, float lz_penalty,
+                 float lz_center, float l2_penalty, float* diff, float* nvalid, void* stream) {
+  if (!h || !e_l || !obs || !stats || !diff || !nvalid) return fail(DH_EINVAL, "null argument");
+  if (B < 1) return fail(DH_EINVAL, "dh_loss_diff needs B >= 1");
+  launch_loss_diff(e_l, obs, B, stats, lz_penalty, lz_center, l2_penalty, diff, nvalid, (hipStream_t)stream);
   return check_launch();
 }
 

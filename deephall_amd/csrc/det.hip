@@ -795,6 +795,141 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
   }
 }
 
+
+// ------------------------------------------------------------------ backward (parameter gradient)
+// log psi = J + log sum_k det Phi_k (psiformer.py:72-76, 91).  For the per-walker cotangent
+// c = ct.re + i ct.im of (Re log psi, Im log psi):
+//   d log psi / d Phi_k[i][j] = w_k inv_k[j][i],  w_k = det Phi_k / sum_k det Phi_k
+//   G_k = c conj(w_k inv_k^T)   (dL/dRe Phi = Re G, dL/dIm Phi = Im G)
+//   dF[i, (blk_i, re|im, m, j, k)] = G_k[i][j] conj(env[i][m])   (blocks.py:64-68)
+//   jg = ct.re dJ/d(alpha_par, alpha_anti),  dJ/dalpha = -c alpha (alpha + 2 r) / (alpha + r)^2
+// One 64-thread workgroup per walker: pass 1 LU of every Phi_k (the log-dets), pass 2
+// Gauss-Jordan inverse of each Phi_k and the owned columns of dF; the other spin block's
+// and the padding columns are written 0.
+__global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+                                                     const float* __restrict__ jas, const float* __restrict__ norm,
+                                                     const float* __restrict__ ct, float* __restrict__ dF,
+                                                     float* __restrict__ jg, int N, int n_up, int M, int K,
+                                                     int orb_cols) {
+  extern __shared__ float sm_raw[];
+  cf* E0 = reinterpret_cast<cf*>(sm_raw);  // [N][M]
+  cf* A = E0 + N * M;                      // [N][2N]
+  cf* fac = A + 2 * N * N;                 // [N]
+  cf* ld = fac + N;                        // [K]
+  cf* logdet = ld + K;
+  cf* wk = logdet + 1;                     // [K]
+  int* piv = reinterpret_cast<int*>(wk + K);
+  float* cart = reinterpret_cast<float*>(piv + 2);  // [N][3]
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const FView F{Fp, ldF, M, N, K};
+  const int MNK = M * N * K;
+  for (int idx = tid; idx < N * M; idx += nt) {
+    const int i = idx / M, p = idx % M;
+    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
+  }
+  for (int i = tid; i < N; i += nt) {
+    float st, ct_, sp, cp;
+    sincosf(x[2 * (b * N + i)], &st, &ct_);
+    sincosf(x[2 * (b * N + i) + 1], &sp, &cp);
+    cart[3 * i] = st * cp;
+    cart[3 * i + 1] = st * sp;
+    cart[3 * i + 2] = ct_;
+  }
+  // columns of dF this walker's rows do not own: the other spin block, the padding
+  for (int idx = tid; idx < N * ldF; idx += nt) {
+    const int i = idx / ldF, col = idx - (idx / ldF) * ldF;
+    const int blk_i = (i >= n_up && n_up > 0) ? 1 : 0;
+    const bool own = col < orb_cols && col / (2 * MNK) == blk_i;
+    if (!own) dF[((size_t)b * N + i) * ldF + col] = 0.f;
+  }
+  const float cr = ct[2 * b], ci = ct[2 * b + 1];
+  __syncthreads();
+  // Jastrow parameter derivatives (double, reduced over the wave)
+  {
+    double gp = 0.0, ga = 0.0;
+    const double ap = jas[0], aa = jas[1];
+    for (int q = tid; q < N * N; q += nt) {
+      const int i = q / N, j = q - (q / N) * N;
+      if (j <= i) continue;
+      const double dx = (double)cart[3 * j] - cart[3 * i], dy = (double)cart[3 * j + 1] - cart[3 * i + 1],
+                   dz = (double)cart[3 * j + 2] - cart[3 * i + 2];
+      const double r = sqrt(dx * dx + dy * dy + dz * dz);
+      const bool same = (i < n_up) == (j < n_up);
+      const double al = same ? ap : aa, cst = same ? 0.25 : 0.5;
+      const double g = -cst * al * (al + 2.0 * r) / ((al + r) * (al + r));
+      if (same)
+        gp += g;
+      else
+        ga += g;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      gp += __shfl_xor(gp, o, 64);
+      ga += __shfl_xor(ga, o, 64);
+    }
+    if (tid == 0) {
+      jg[2 * b] = (float)(cr * gp);
+      jg[2 * b + 1] = (float)(cr * ga);
+    }
+  }
+  auto build = [&](int k, int lda) {
+    for (int idx = tid; idx < N * N; idx += nt) {
+      const int i = idx / N, j = idx % N;
+      const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+      const size_t row = (size_t)b * N + i;
+      cf acc{0.f, 0.f};
+      for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
+      A[i * lda + j] = acc;
+      if (lda > N) A[i * lda + N + j] = cf{i == j ? 1.f : 0.f, 0.f};
+    }
+    __syncthreads();
+  };
+  // pass 1: log det of every determinant -> softmax weights w_k
+  if (K > 1) {
+    for (int k = 0; k < K; ++k) {
+      build(k, N);
+      eliminate(A, N, N, N, false, fac, piv, logdet);
+      if (tid == 0) ld[k] = *logdet;
+      __syncthreads();
+    }
+    if (tid == 0) {
+      float lmax = -INFINITY;
+      for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, ld[k].re);
+      cf z{0.f, 0.f};
+      for (int k = 0; k < K; ++k) {
+        const float mag = expf(ld[k].re - lmax);
+        z += cf{mag * cosf(ld[k].im), mag * sinf(ld[k].im)};
+      }
+      for (int k = 0; k < K; ++k) {
+        const float mag = expf(ld[k].re - lmax);
+        wk[k] = cdiv(cf{mag * cosf(ld[k].im), mag * sinf(ld[k].im)}, z);
+      }
+    }
+  } else if (tid == 0) {
+    wk[0] = cf{1.f, 0.f};
+  }
+  __syncthreads();
+  // pass 2: inverse of each Phi_k, owned dF columns
+  for (int k = 0; k < K; ++k) {
+    build(k, 2 * N);
+    eliminate(A, 2 * N, N, 2 * N, true, fac, piv, logdet);
+    const cf w = wk[k];
+    for (int idx = tid; idx < N * M * N; idx += nt) {
+      const int i = idx / (M * N), rem = idx - i * (M * N), p = rem / N, j = rem - (rem / N) * N;
+      const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+      const cf f = w * A[j * 2 * N + N + i];  // d log psi / d Phi_k[i][j]
+      // G = c conj(f); dF = G conj(env)
+      const cf G{cr * f.re + ci * f.im, ci * f.re - cr * f.im};
+      const cf e = E0[i * M + p];
+      const cf v{G.re * e.re + G.im * e.im, G.im * e.re - G.re * e.im};
+      const size_t rowoff = ((size_t)b * N + i) * ldF;
+      const int off = p * N * K + j * K + k;
+      dF[rowoff + (size_t)(blk * 2) * MNK + off] = v.re;
+      dF[rowoff + (size_t)(blk * 2 + 1) * MNK + off] = v.im;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void potential_kernel(const float* __restrict__ x, float* __restrict__ pe, int nw, int N, float Q,
                                  float radius, int interaction) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -828,6 +963,15 @@ void launch_det_value(const Dims& d, const float* F, const float* x, const float
   const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 3 * d.N) * sizeof(float);
   hipLaunchKernelGGL(det_value_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N,
                      d.n_up, d.M, d.K);
+}
+
+void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
+                    const float* ct, float* dF, float* jg, int nw, hipStream_t s) {
+  const size_t bytes =
+      (size_t)(2 * d.N * d.M + 4 * d.N * d.N + 2 * d.N + 4 * d.K + 2 + 4 + 3 * d.N) * sizeof(float);
+  ensure_smem(det_bwd_kernel, bytes);
+  hipLaunchKernelGGL(det_bwd_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, ct, dF, jg, d.N,
+                     d.n_up, d.M, d.K, d.orb_cols);
 }
 
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,

@@ -27,6 +27,10 @@ struct Dims {
 // Device pointers into the packed parameter buffer.
 struct LayerParams {
   const float *Wqkv, *bqkv, *Wol, *bol, *ln1, *Wm, *bm, *ln2;
+  // backward (x^T-side) copies of the same weights for dX = dY W^T: split-bf16 planes of the
+  // untransposed W (x6 path) or W^T [ncols][D] (exact-f32 path)
+  const uint16_t *WqkvB, *WolB, *WmB;
+  const float *WqkvBT, *WolBT, *WmBT;
   const float *WqkvT, *WolT, *WmT;  // transposed copies [ncols pad 256][D] for the NT GEMM
   const uint16_t *WqkvP, *WolP, *WmP;  // split-bf16 planes [3][x6_plane_rows(ncols)][D] (gemm_x6)
 };
@@ -34,9 +38,11 @@ struct Params {
   const float* W0;
   LayerParams layer[16];
   const float *Worb, *borb, *jastrow;
-  const float* W0qkv;  // [4][3D] = W0 @ Wqkv of layer 0 (folded on the host)
+  const float* W0qkv;  // [4][3D] = W0 @ Wqkv of layer 0 (folded at packing)
   const float* WorbT;  // [orb_cols pad 256][D]
   const uint16_t* WorbP;  // split-bf16 planes of Worb
+  const uint16_t* WorbB;  // backward planes (untransposed Worb [D][ld_orb])
+  const float* WorbBT;    // backward exact-f32 copy Worb^T [ld_orb][D]
 };
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
@@ -143,7 +149,37 @@ void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const fl
 void launch_lp_from_logpsi(const float* logpsi, float* lp, int32_t* n_acc, int nw, hipStream_t s);
 
 // stats.hip
-void launch_stats(const float* e_l, const float* obs, const int32_t* n_acc, int B, int steps, float* out,
-                  float* scratch, hipStream_t s);
+void launch_stats(const float* e_l, const float* obs, const int32_t* n_acc, int B, int steps, int penalties,
+                  float* out, hipStream_t s);
+// g: device pointer to the reduced stats; diff [B][2]; nvalid [1]
+void launch_loss_diff(const float* e_l, const float* obs, int B, const float* g, float lz_penalty, float lz_center,
+                      float l2_penalty, float* diff, float* nvalid, hipStream_t s);
+
+// grad.hip: reverse mode of log psi w.r.t. the parameters (see the file header)
+constexpr int kGradChunk = 512;       // rows per weight-gradient partial
+constexpr int kLnRowsPerBlock = 64;   // rows per LayerNorm-backward block (one partial each)
+int grad_chunks(int rows);
+int ln_bwd_blocks(int rows);
+void launch_ln_fwd(const float* a, const float* z, const float* ln, float* out, int rows, int D, hipStream_t s);
+void launch_ln_bwd(const float* a, const float* z, const float* ln, const float* dy, const float* dres, float* da,
+                   float* dz, float* pg, int rows, int D, hipStream_t s);
+void launch_attn_bwd(const Dims& d, const float* qkv, const float* dO, float* dqkv, int nw, hipStream_t s);
+void launch_tn_partial(const float* X, int ldx, const float* Y, int ldy, int rows, int M, int Nc, float* P,
+                       hipStream_t s);
+void launch_colsum_partial(const float* Y, int ldy, int rows, int Nc, float* P, hipStream_t s);
+void launch_w0_partial(const Dims& d, const float* geo, const float* Y, int ldy, int rows, float* P, hipStream_t s);
+// out[r * ldo + c] = scale * sum_ch P[ch * stride + r * ldp + c] (+ out if acc), r < nr, c < nc
+void launch_reduce2d(const float* P, int nchunk, size_t stride, int ldp, int nr, int nc, float* out, int ldo,
+                     float scale, int acc, hipStream_t s);
+void launch_small_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
+                       int ldc, int acc, hipStream_t s);
+void launch_copy2d(const float* src, int lds, float* dst, int ldd, int nr, int nc, hipStream_t s);
+void launch_cotangent(const float* diff, const float* nvalid, int B, int part, float* ct, hipStream_t s);
+void launch_adam(float* p, const float* g, float* mu, float* nu, size_t n, float lr, float b1, float b2, float eps,
+                 int step, hipStream_t s);
+// det.hip: backward of log psi = J + log sum_k det Phi_k for per-walker cotangents ct[nw][2]:
+// dF [nw*N][ld_orb] (all columns written) and jg[nw][2] = ct.re * dJ / d(ee_par, ee_anti)
+void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
+                    const float* ct, float* dF, float* jg, int nw, hipStream_t s);
 
 }  // namespace dh

@@ -5,8 +5,8 @@ evaluates E_L on this rank's walkers (dh_local_energy), reduces them on the
 device (dh_energy_stats: nanmean, IQR-clipped nanmean with LOCAL quantiles as in
 loss.py:30-38, observable means) and averages over ranks with ONE packed
 all-reduce (the reference issues one ``pmean`` per statistic, loss.py:68-91).
-Returns (LossStats, None): the parameter-gradient half (loss.py:53-64, 93-108)
-is the next row of the build plan, not this hot path.
+The parameter-gradient half (loss.py:53-64, 93-108) runs as reverse mode in the HIP
+library (dh_loss_diff -> dh_grad_cotangent -> dh_logpsi_vjp) and a second all-reduce.
 """
 
 from __future__ import annotations
@@ -20,8 +20,9 @@ from .hamiltonian import _run_local_energy
 from .mcmc import resolve_network
 from .networks.psiformer import _ptr, _stream, get_handle
 
-# packed all-reduce layout (first 12 entries of dh_energy_stats + count)
-_PACK = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
+# packed all-reduce: every DH_STAT_* entry (16 floats; the clipped Lz^2 / Lz / L^2 means
+# are 0 unless the penalties are on)
+_NPACK = _lib.DH_NSTATS
 
 
 class LossMode(enum.Enum):
@@ -30,23 +31,25 @@ class LossMode(enum.Enum):
     SR_F_VECTOR = enum.auto()
 
 
-def device_stats(net, e_l, obs, n_accept=None, steps=1):
+def device_stats(net, e_l, obs, n_accept=None, steps=1, penalties=False):
     """dh_energy_stats on this rank: float32 [16] device tensor (DH_STAT_* layout)."""
     h = get_handle(net.spec, e_l.device)
     out = torch.empty(_lib.DH_NSTATS, dtype=torch.float32, device=e_l.device)
     _lib.check(
         h.lib.dh_energy_stats(
-            h.h, _ptr(e_l), _ptr(obs), _ptr(n_accept), e_l.shape[0], int(steps), _ptr(out), None, 0, _stream(e_l.device)
+            h.h, _ptr(e_l), _ptr(obs), _ptr(n_accept), e_l.shape[0], int(steps), int(bool(penalties)), _ptr(out),
+            _stream(e_l.device),
         )
     )
     return out
 
 
-def reduce_stats(local: torch.Tensor) -> dict:
-    """One all-reduce of the packed device-local stats -> LossStats dict (0-d tensors)."""
-    g = constants.pmean(local[: len(_PACK)])
+def reduce_stats(local: torch.Tensor, raw: bool = False):
+    """One all-reduce of the packed device-local stats -> LossStats dict (0-d tensors).
+    ``raw=True`` also returns the reduced packed vector (device, DH_STAT_* layout)."""
+    g = constants.pmean(local[:_NPACK])
     energy = torch.complex(g[0], g[1])
-    return {
+    out = {
         "energy": energy,
         "clipped_energy": torch.complex(g[2], g[3]),
         "variance": g[4] - g[0] * g[0],  # pmean(nanmean(Re E^2)) - Re(energy)^2 (loss.py:91)
@@ -57,18 +60,60 @@ def reduce_stats(local: torch.Tensor) -> dict:
         "angular_momentum_square": g[10],
         "pmove": g[11],
     }
+    return (out, g) if raw else out
 
 
-def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_DIFF):
-    if mode != LossMode.ENERGY_DIFF:
-        raise NotImplementedError("parameter gradients (loss.py:53-64) are not on the MI355X hot path yet")
+def loss_diff(net, e_l, obs, gstats, lz_penalty=0.0, lz_center=0.0, l2_penalty=0.0):
+    """dh_loss_diff: diff = iqr_clip(E_L - <E_L>_clip + penalties) (loss.py:75-89) with the
+    reduced clipped means ``gstats`` (device, DH_STAT_* layout).  Returns (diff [B,2] f32,
+    nvalid [1] f32 = walkers with a non-NaN diff)."""
+    h = get_handle(net.spec, e_l.device)
+    B = e_l.shape[0]
+    diff = torch.empty(B, 2, dtype=torch.float32, device=e_l.device)
+    nvalid = torch.empty(1, dtype=torch.float32, device=e_l.device)
+    _lib.check(
+        h.lib.dh_loss_diff(
+            h.h, _ptr(e_l), _ptr(obs), B, _ptr(gstats), float(lz_penalty), float(lz_center), float(l2_penalty),
+            _ptr(diff), _ptr(nvalid), _stream(e_l.device),
+        )
+    )
+    return diff, nvalid
+
+
+def grad_cotangent(diff, nvalid, part=0):
+    """dh_grad_cotangent: per-walker weights of 2 nanmean(conj(d log psi) diff) (loss.py:59-64);
+    part 0 = its real part (ENERGY_GRAD), part 1 = its imaginary part."""
+    B = diff.shape[0]
+    ct = torch.empty(B, 2, dtype=torch.float32, device=diff.device)
+    _lib.check(_lib.load().dh_grad_cotangent(_ptr(diff), _ptr(nvalid), B, int(part), _ptr(ct), _stream(diff.device)))
+    return ct
+
+
+def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_GRAD):
+    """loss.py:47-110.  ``loss_and_grad(params, data) -> (LossStats, aux)`` where aux is
+    diff [B] complex (ENERGY_DIFF), the real parameter gradient (ENERGY_GRAD, a ParamTree)
+    or the complex one ({name: complex tensor}, SR_F_VECTOR).  Every statistic and the
+    gradient are averaged over ranks: one packed all-reduce of the statistics, one of the
+    gradient (the reference's Adam path skips the latter, SURVEY.md finding 9)."""
     net = resolve_network(network)
+    pen = (float(system.lz_penalty), float(system.lz_center), float(system.l2_penalty))
+    penalties = pen[0] != 0.0 or pen[2] != 0.0
 
     def loss_and_grad(params, data, n_accept=None, steps=1):
         e_l, obs = _run_local_energy(net, params, data)
-        local = device_stats(net, e_l, obs, n_accept, steps)
-        stats = reduce_stats(local)
+        local = device_stats(net, e_l, obs, n_accept, steps, penalties=penalties)
+        stats, g = reduce_stats(local, raw=True)
         loss_and_grad.last = (e_l, obs)
-        return stats, None
+        diff, nvalid = loss_diff(net, e_l, obs, g, *pen)
+        if mode == LossMode.ENERGY_DIFF:
+            return stats, torch.complex(diff[:, 0], diff[:, 1])
+        grad = net.vjp(params, data, grad_cotangent(diff, nvalid, 0))
+        constants.pmean_(grad.flat)
+        if mode == LossMode.ENERGY_GRAD:
+            return stats, grad
+        gim = net.vjp(params, data, grad_cotangent(diff, nvalid, 1))
+        constants.pmean_(gim.flat)
+        return stats, {k: torch.complex(grad[k], gim[k]) for k in grad}
 
+    loss_and_grad.network = net
     return loss_and_grad

@@ -11,9 +11,9 @@ orbital_type) and its two entry points:
   ``model.apply`` is per walker and vmapped by its callers (train.py:69); the
   native kernels are batched, so the batch axis is explicit here.
 
-All arithmetic runs in the HIP library (include/deephall_amd.h); this module
-only packs parameters into the layout of ``dh_param_layout`` and manages the
-per-device handle and workspace.
+All arithmetic runs in the HIP library (include/deephall_amd.h); this module only
+flattens the parameter tree into the ``dh_ref_layout`` buffer (the library packs
+it on the device) and manages the per-device handle and workspace.
 """
 
 from __future__ import annotations
@@ -29,6 +29,7 @@ import torch
 from .. import _lib
 
 _HANDLES: dict = {}
+VJP_WORKSPACE_BYTES = 16 << 30  # walkers beyond this go through in chunks
 
 
 def _ptr(t: torch.Tensor | None):
@@ -89,11 +90,13 @@ class NativeHandle:
         self.h = C.c_void_p()
         cfg = spec.to_c()
         _lib.check(self.lib.dh_create(C.byref(cfg), C.byref(self.h)))
-        nseg = self.lib.dh_param_layout(self.h, None, 0)
+        nseg = self.lib.dh_ref_layout(self.h, None, 0)
         offs = (C.c_size_t * (nseg + 1))()
-        self.lib.dh_param_layout(self.h, offs, nseg + 1)
-        self.offsets = [int(o) for o in offs]
-        self.nparams = self.offsets[-1]
+        self.lib.dh_ref_layout(self.h, offs, nseg + 1)
+        self.ref_offsets = [int(o) for o in offs]
+        if self.ref_offsets != ref_offsets(spec):
+            raise RuntimeError("dh_ref_layout disagrees with the Python parameter tree")
+        self.nref = self.ref_offsets[-1]
         self.ws = {}  # one workspace per HIP stream (walker groups may run on parallel streams)
         self._params_key = None
         self.set_gemm_mode(_GEMM_MODE)
@@ -121,12 +124,14 @@ class NativeHandle:
             self.ws[sid] = ws
         return ws
 
-    def set_params(self, packed: torch.Tensor, key):
+    def set_params_ref(self, flat: torch.Tensor, key):
+        """Upload the flat reference tree; the library packs it on the device (folds,
+        transposes, split-bf16 planes: dh_set_params_ref)."""
         if self._params_key == key:
             return
-        assert packed.numel() == self.nparams and packed.dtype == torch.float32 and packed.is_cuda
-        _lib.check(self.lib.dh_set_params(self.h, _ptr(packed), self.nparams, _stream(self.device)))
-        self._packed = packed  # keep alive while the copy is in flight
+        assert flat.numel() == self.nref and flat.dtype == torch.float32 and flat.is_cuda
+        _lib.check(self.lib.dh_set_params_ref(self.h, _ptr(flat), self.nref, _stream(self.device)))
+        self._flat = flat  # keep alive while the copy is in flight
         self._params_key = key
 
 
@@ -203,12 +208,53 @@ def param_shapes(spec: NetworkSpec) -> dict:
     return s
 
 
-def init_params(spec: NetworkSpec, seed: int, device="cpu") -> dict:
+def ref_offsets(spec: NetworkSpec) -> list:
+    """Float offsets of the flat reference tree (dh_ref_layout): param_shapes order,
+    64-float aligned segments; the last entry is the total."""
+    offs, o = [], 0
+    for shape in param_shapes(spec).values():
+        offs.append(o)
+        o += (int(np.prod(shape)) + 63) // 64 * 64
+    offs.append(o)
+    return offs
+
+
+class ParamTree(dict):
+    """{Flax path: tensor} whose tensors are views into ONE flat float32 buffer in the
+    dh_ref_layout order (``.flat``).  Optimizers update ``.flat`` in place; the kernels
+    upload it as is."""
+
+    flat: torch.Tensor
+
+    @classmethod
+    def zeros(cls, spec: NetworkSpec, device) -> "ParamTree":
+        offs = ref_offsets(spec)
+        flat = torch.zeros(offs[-1], dtype=torch.float32, device=device)
+        t = cls()
+        for (name, shape), o in zip(param_shapes(spec).items(), offs):
+            t[name] = flat[o : o + int(np.prod(shape))].view(shape)
+        t.flat = flat
+        return t
+
+    def is_packed_view(self, spec: NetworkSpec) -> bool:
+        """True while every leaf is still the original view into ``flat``."""
+        flat = getattr(self, "flat", None)
+        if flat is None:
+            return False
+        base = flat.data_ptr()
+        for (name, _), o in zip(param_shapes(spec).items(), ref_offsets(spec)):
+            v = self.get(name)
+            if v is None or v.data_ptr() != base + 4 * o or not v.is_contiguous():
+                return False
+        return True
+
+
+def init_params(spec: NetworkSpec, seed: int, device="cpu") -> ParamTree:
     """Flax-default initialisation: lecun_normal (truncated to 2 sigma) kernels
     (fan_in = input features; H*dh for the attention output), zero biases,
     LayerNorm scale 1, Jastrow alphas 1 (blocks.py:92,100)."""
     rng = np.random.default_rng(seed)
-    out = {}
+    out = ParamTree.zeros(spec, device)
     for name, shape in param_shapes(spec).items():
         if name.endswith("/kernel"):
             fan_in = shape[0] * shape[1] if "out/kernel" in name else shape[0]
@@ -223,77 +269,30 @@ def init_params(spec: NetworkSpec, seed: int, device="cpu") -> dict:
             arr = np.ones(shape)
         else:
             arr = np.zeros(shape)
-        out[name] = torch.tensor(arr, dtype=torch.float32, device=device)
+        out[name].copy_(torch.tensor(arr, dtype=torch.float32))
     return out
 
 
-def pack_params(spec: NetworkSpec, params: dict, offsets: list, device) -> torch.Tensor:
-    """Packed float32 device buffer in the dh_param_layout order (include/deephall_amd.h).
-
-    The attention output projection and the following bias-free Dense
-    (psiformer.py:44-45) are folded into one matrix Wol = Wo @ Wl (computed in
-    float64), bol = bo @ Wl.
-    """
+def flat_params(spec: NetworkSpec, params, device) -> torch.Tensor:
+    """The flat reference-layout buffer of a parameter dict: ``params.flat`` when the dict
+    is an intact ParamTree on ``device``, else a float32 copy assembled segment by segment."""
+    if isinstance(params, ParamTree) and params.is_packed_view(spec) and params.flat.device == torch.device(device):
+        return params.flat
     P = flatten_params(params)
-    D, M, N, K = spec.D, spec.M, spec.nelec, spec.ndets
-    dev = torch.device(device)
-    buf = torch.zeros(offsets[-1], dtype=torch.float32, device=dev)
-    f64 = lambda name: P[name].detach().to(dev, torch.float64)  # noqa: E731
-    seg = 0
-
-    def put(t):
-        nonlocal seg
-        flat = t.reshape(-1).to(torch.float32)
-        size = offsets[seg + 1] - offsets[seg]
-        assert flat.numel() <= size, (seg, flat.numel(), size)
-        buf[offsets[seg] : offsets[seg] + flat.numel()] = flat
-        seg += 1
-
-    p = "PsiformerLayers_0/"
-    put(f64(p + "Dense_0/kernel"))
-    for l in range(spec.num_layers):
-        mha = p + f"MultiHeadAttention_{l}/"
-        wq = torch.cat([f64(mha + n + "/kernel").reshape(D, D) for n in ("query", "key", "value")], 1)
-        bq = torch.cat([f64(mha + n + "/bias").reshape(D) for n in ("query", "key", "value")])
-        wl = f64(p + f"Dense_{2 * l + 1}/kernel")
-        put(wq)
-        put(bq)
-        put(f64(mha + "out/kernel").reshape(D, D) @ wl)
-        put(f64(mha + "out/bias") @ wl)
-        put(torch.stack([f64(p + f"LayerNorm_{2 * l}/scale"), f64(p + f"LayerNorm_{2 * l}/bias")]))
-        put(f64(p + f"Dense_{2 * l + 2}/kernel"))
-        put(f64(p + f"Dense_{2 * l + 2}/bias"))
-        put(torch.stack([f64(p + f"LayerNorm_{2 * l + 1}/scale"), f64(p + f"LayerNorm_{2 * l + 1}/bias")]))
-    ob = "Orbitals_0/featured_orbitals/"
-    nblk = sum(1 for n in spec.nspins if n > 0)
-    MNK = M * N * K
-    cols = nblk * 2 * MNK
-    ld = ((cols + 127) // 128) * 128
-    W = torch.zeros(D, ld, dtype=torch.float64, device=dev)
-    bvec = torch.zeros(ld, dtype=torch.float64, device=dev)
-    for i in range(2 * nblk):  # (blk, part) order: DenseGeneral_{2 blk + part}
-        W[:, i * MNK : (i + 1) * MNK] = f64(ob + f"DenseGeneral_{i}/kernel").reshape(D, MNK)
-        bvec[i * MNK : (i + 1) * MNK] = f64(ob + f"DenseGeneral_{i}/bias").reshape(MNK)
-    put(W)
-    put(bvec)
-    jp = P.get("Jastrow_0/ee_par")
-    ja = P.get("Jastrow_0/ee_anti")
-    put(
-        torch.tensor(
-            [float(jp.reshape(-1)[0]) if jp is not None else 1.0, float(ja.reshape(-1)[0]) if ja is not None else 1.0],
-            dtype=torch.float64,
-            device=dev,
-        )
-    )
-    # layer-1 q|k|v projection folded into the input map: W0 @ Wqkv (float64), [4][3D]
-    if spec.num_layers > 0:
-        mha = p + "MultiHeadAttention_0/"
-        wq0 = torch.cat([f64(mha + n + "/kernel").reshape(D, D) for n in ("query", "key", "value")], 1)
-        put(f64(p + "Dense_0/kernel") @ wq0)
-    else:
-        seg += 1
-    assert seg == len(offsets) - 1
-    return buf
+    offs = ref_offsets(spec)
+    flat = torch.zeros(offs[-1], dtype=torch.float32, device=device)
+    for (name, shape), o in zip(param_shapes(spec).items(), offs):
+        n = int(np.prod(shape))
+        if name not in P:
+            if name.startswith("Jastrow"):  # optional leaves (blocks.py:92,100): alpha = 1
+                flat[o] = 1.0
+                continue
+            raise KeyError(f"parameter {name} missing")
+        t = P[name]
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"parameter {name}: shape {tuple(t.shape)} != {tuple(shape)}")
+        flat[o : o + n] = t.detach().reshape(-1).to(device=device, dtype=torch.float32)
+    return flat
 
 
 class Psiformer:
@@ -323,10 +322,11 @@ class Psiformer:
             interaction_strength=float(lam),
             interaction_type=str(getattr(itype, "value", itype)),
         )
-        self._pack_cache = {}
+        self._flat_cache = {}
+        self._epoch = 0
 
     # ---- reference-compatible entry points
-    def init(self, key, data=None, device=None) -> dict:
+    def init(self, key, data=None, device=None) -> ParamTree:
         seed = int(getattr(key, "seed", key))
         if device is None:
             device = data.device if isinstance(data, torch.Tensor) else ("cuda" if torch.cuda.is_available() else "cpu")
@@ -345,6 +345,26 @@ class Psiformer:
 
     __call__ = apply
 
+    def vjp(self, params, data: torch.Tensor, ct: torch.Tensor, out: "ParamTree | None" = None,
+            logpsi: torch.Tensor | None = None) -> "ParamTree":
+        """Parameter gradient sum_b ct[b,0] dRe log psi_b/dp + ct[b,1] dIm log psi_b/dp by
+        reverse mode in the HIP library (dh_logpsi_vjp), as a ParamTree of float32 views
+        (the reference's jax.grad of network(params, x).real / .imag, loss.py:53-58)."""
+        h = self.prepare(params, data.device)
+        x = self._check_walkers(data)
+        B = x.shape[0]
+        ct = ct.to(device=x.device, dtype=torch.float32).contiguous()
+        if tuple(ct.shape) != (B, 2):
+            raise ValueError(f"cotangents must be [{B}, 2]")
+        if out is None:
+            out = ParamTree.zeros(self.spec, x.device)
+        need = h.lib.dh_vjp_workspace_bytes(h.h, B)
+        one = h.lib.dh_vjp_workspace_bytes(h.h, 1)
+        ws = h.workspace(max(min(need, VJP_WORKSPACE_BYTES), one))
+        _lib.check(h.lib.dh_logpsi_vjp(h.h, _ptr(x), B, _ptr(ct), _ptr(out.flat), _ptr(logpsi), _ptr(ws), ws.numel(),
+                                       _stream(x.device)))
+        return out
+
     # ---- plumbing
     def _check_walkers(self, data: torch.Tensor) -> torch.Tensor:
         if data.dim() != 3 or data.shape[1] != self.spec.nelec or data.shape[2] != 2:
@@ -355,10 +375,23 @@ class Psiformer:
 
     def prepare(self, params, device) -> NativeHandle:
         h = get_handle(self.spec, device)
-        flat = flatten_params(params) if isinstance(params, dict) else params
-        key = (id(params), tuple((id(v), v._version) for v in flat.values()) if isinstance(flat, dict) else None)
-        if key not in self._pack_cache:
-            self._pack_cache.clear()
-            self._pack_cache[key] = pack_params(self.spec, flat, h.offsets, h.device)
-        h.set_params(self._pack_cache[key], key)
+        if isinstance(params, ParamTree) and params.is_packed_view(self.spec) and params.flat.device == h.device:
+            flat = params.flat
+            # in-place updates through any view bump the shared version counter; updates
+            # written by the optimizer kernels call invalidate()
+            key = ("flat", flat.data_ptr(), flat._version, self._epoch)
+        else:
+            P = flatten_params(params) if isinstance(params, dict) else params
+            key = (id(params), tuple((id(v), v.data_ptr(), v._version) for v in P.values()), self._epoch)
+            if key not in self._flat_cache:
+                self._flat_cache.clear()
+                self._flat_cache[key] = flat_params(self.spec, P, h.device)
+            flat = self._flat_cache[key]
+        h.set_params_ref(flat, key)
         return h
+
+    def invalidate(self):
+        """Force the next call to re-upload the parameters (after updates that bypass the
+        tensors' version counters: optimizer kernels, ``p.data.copy_``)."""
+        self._flat_cache.clear()
+        self._epoch += 1

@@ -83,7 +83,7 @@ def setup_mcmc(cfg: Config, model):
     return step, pmoves
 
 
-def make_vmc_iteration(model, batch_per_device: int, steps: int, groups: int = 2):
+def make_vmc_iteration(model, batch_per_device: int, steps: int, groups: int = 1):
     """The device work of one VMC iteration (train.py:128-140 before the statistics):
     ``mcmc_step`` then the local energy, for this rank's walkers.
 
@@ -91,9 +91,9 @@ def make_vmc_iteration(model, batch_per_device: int, steps: int, groups: int = 2
     the batch is cut into ``groups`` contiguous walker groups, each run start to finish
     (its MCMC moves, then its local energies) on its own HIP stream; the results are
     bit-identical to one group (same walkers, same random numbers, same arithmetic).
-    Measured on MI355X at C2 (4096 walkers): 2 groups 12.8 ms vs 1 group 10.75 ms per
-    iteration — co-scheduled kernels of two groups slow each other down more than they
-    fill idle CUs — so the default is one group; the option stays for smaller kernels.
+    Every side stream waits on the caller's stream ONCE, before any group's work is
+    queued, so the groups really run concurrently (DESIGN.md §7.1 has the measurement).
+    The default is one group.
 
     Returns ``iteration(params, data, key, width) -> (data, e_l [B,2], obs [B,8],
     n_accept [B])``; data is updated in place.
@@ -109,11 +109,12 @@ def make_vmc_iteration(model, batch_per_device: int, steps: int, groups: int = 2
         while len(side) < groups - 1:
             side.append(torch.cuda.Stream(data.device))
         base = constants.rank() * B
+        model.prepare(params, data.device)  # any parameter upload is queued on `main` first
+        for s in side[: groups - 1]:
+            s.wait_stream(main)  # inputs ready; nothing of this iteration is queued yet
         outs, off = [], 0
         for g, n in enumerate(sizes):
             s = main if g == 0 else side[g - 1]
-            if g > 0:
-                s.wait_stream(main)
             with torch.cuda.stream(s):
                 d = data[off : off + n]
                 mcmc[g](params, d, key, width, reduce=False, walker_offset=base + off)

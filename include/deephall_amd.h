@@ -103,6 +103,44 @@ int dh_param_layout(const dh_handle* h, size_t* offsets, int n);
  * handle.  `count` must equal the total from dh_param_layout. */
 int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream);
 
+/* Reference parameter tree, flattened (SURVEY.md Appendix B names, Flax order):
+ *   0                 PsiformerLayers_0/Dense_0/kernel [4][D]
+ *   per layer l (15 segments, base 1+15l):
+ *     MultiHeadAttention_l/{query,key,value}/{kernel [D][H*dh], bias [H*dh]}  (+0..+5)
+ *     MultiHeadAttention_l/out/{kernel [H*dh][D], bias [D]}                   (+6, +7)
+ *     Dense_{2l+1}/kernel [D][D]; LayerNorm_{2l}/{scale, bias} [D]             (+8..+10)
+ *     Dense_{2l+2}/{kernel [D][D], bias [D]}; LayerNorm_{2l+1}/{scale, bias}   (+11..+14)
+ *   1+15L+2i, +1      Orbitals_0/featured_orbitals/DenseGeneral_i/{kernel [D][M*N*K],
+ *                     bias [M*N*K]}, i < 2 * (spin blocks)
+ *   then              Jastrow_0/ee_par [1], Jastrow_0/ee_anti [1]
+ * Segments are 64-float aligned.  Returns the segment count; offsets[nseg] = total floats.
+ * Parameter gradients (dh_logpsi_vjp) use the same layout. */
+int dh_ref_layout(const dh_handle* h, size_t* offsets, int n);
+/* Upload the reference tree (device pointer, `count` = total floats of dh_ref_layout) and
+ * pack it on the device: concatenations, zero padding, and the folds Wo Wl, bo Wl,
+ * W0 Wqkv (double-accumulated), transposed / split-bf16 copies.  Replaces the host
+ * packing of dh_set_params; required by dh_logpsi_vjp. */
+int dh_set_params_ref(dh_handle* h, const float* ref, size_t count, void* stream);
+
+/* Parameter gradient by reverse mode (loss.py:53-64, 93-108 with jax.grad of the network):
+ *   grad = sum_b ct[b][0] d Re log psi_b / dp + ct[b][1] d Im log psi_b / dp
+ * ct [B][2] per-walker cotangents (dh_grad_cotangent), grad [dh_ref_layout total] f32,
+ * logpsi [B][2] optional (NULL) log psi of the walkers from the same forward pass.
+ * Processes walkers in chunks sized to the workspace (dh_vjp_workspace_bytes per chunk). */
+size_t dh_vjp_workspace_bytes(const dh_handle* h, int batch);
+int dh_logpsi_vjp(dh_handle* h, const float* x, int B, const float* ct, float* grad, float* logpsi, void* ws,
+                  size_t ws_bytes, void* stream);
+/* Cotangents of the gradient estimator 2 nanmean(conj(d log psi) diff) (loss.py:59-64):
+ * part 0 (its real part, ENERGY_GRAD): ct = 2 (Re diff, Im diff) / n;
+ * part 1 (its imaginary part, SR_F_VECTOR): ct = 2 (Im diff, -Re diff) / n;
+ * n = nvalid[0] (device), NaN diffs give 0. */
+int dh_grad_cotangent(const float* diff, const float* nvalid, int B, int part, float* ct, void* stream);
+/* optax.adam step in place (optimizers/adam.py:24-43): b1, b2, eps as optax, lr = the
+ * schedule value at `step` (config.py:125-137), bias correction with step + 1; NaN
+ * gradients count as 0 (loss.py:64 nan_to_num). */
+int dh_adam_update(float* params, const float* grad, float* mu, float* nu, size_t n, float lr, float b1, float b2,
+                   float eps, int step, void* stream);
+
 /* GEMM arithmetic of the local-energy (2N+5 channel) pass:
  *   DH_GEMM_F32   exact-f32 MFMA (v_mfma_f32_32x32x2_f32), f32 rounding per product;
  *   DH_GEMM_X6    split-bf16 MFMA: each f32 operand split exactly into three bf16 terms,
@@ -150,7 +188,9 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
                     void* stream);
 
 /* Device-local energy statistics (loss.py:66-92 before the pmean).  Writes
- * out[DH_NSTATS] floats: see DH_STAT_* indices.  B <= 32768.  */
+ * out[DH_NSTATS] floats: see DH_STAT_* indices.  Any B >= 1 (quantiles by a radix
+ * select, no sort).  penalties != 0 also computes the clipped Lz^2, Lz, L^2 means that
+ * System.lz_penalty / l2_penalty need (loss.py:76-88); else those entries are 0. */
 #define DH_NSTATS 16
 #define DH_STAT_ENERGY_RE 0    /* nanmean Re E_L                     */
 #define DH_STAT_ENERGY_IM 1    /* nanmean Im E_L                     */
@@ -165,8 +205,20 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
 #define DH_STAT_L2 10          /* mean L^2                           */
 #define DH_STAT_PMOVE 11       /* sum n_accept / (steps * B)         */
 #define DH_STAT_NVALID 12      /* number of non-NaN E_L              */
+#define DH_STAT_CLIPPED_LZ2 13 /* nanmean iqr_clip(Lz^2)  (penalties) */
+#define DH_STAT_CLIPPED_LZ 14  /* nanmean iqr_clip(Lz)    (penalties) */
+#define DH_STAT_CLIPPED_L2 15  /* nanmean iqr_clip(L^2)   (penalties) */
 int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int32_t* n_accept, int B, int steps,
-                    float* out, void* ws, size_t ws_bytes, void* stream);
+                    int penalties, float* out, void* stream);
+
+/* The clipped energy difference that weights the parameter gradient (loss.py:75-89):
+ *   d = E_L - <E_L>_clip + lz_penalty ((Lz^2 - <Lz^2>_clip) - 2 lz_center (Lz - <Lz>_clip))
+ *         + l2_penalty (L^2 - <L^2>_clip),    diff = iqr_clip(d)  (local quantiles)
+ * with the <.>_clip means read from `stats` (device, DH_STAT_* layout, already averaged
+ * over devices).  diff[B][2] (re, im; NaN where E_L is NaN); nvalid[1] = number of
+ * walkers with a non-NaN diff (the nanmean count of loss.py:64). */
+int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const float* stats, float lz_penalty,
+                 float lz_center, float l2_penalty, float* diff, float* nvalid, void* stream);
 
 /* Potential energy only (make_potential, hamiltonian.py:63-80), NOT multiplied by
  * interaction_strength: pe[B]. */

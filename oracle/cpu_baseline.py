@@ -54,6 +54,12 @@ def measure(cfg: R.OracleConfig, steps: int = 10, el_batch: int = 16, fwd_batch:
         t_el += time.perf_counter() - a
         n_el += el_batch
     per_fwd = t_fwd / n_fwd
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), model)
+    except OSError:
+        pass
     per_el = t_el / n_el
     per_iter = per_el + (steps + 1) * per_fwd
     return {
@@ -61,6 +67,8 @@ def measure(cfg: R.OracleConfig, steps: int = 10, el_batch: int = 16, fwd_batch:
         "el_only_per_sec": 1.0 / per_el,
         "walker_steps_per_sec": 1.0 / per_fwd,
         "threads": torch.get_num_threads(),
+        "cpu_model": model,
+        "host_cpus": __import__("os").cpu_count(),
         "sample": f"{n_el} local energies (full autograd Hessian, f32, vmap batch {el_batch}) + "
         f"{n_fwd} forwards (vmap batch {fwd_batch}); {t_el + t_fwd:.1f} s CPU",
     }

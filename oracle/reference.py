@@ -350,6 +350,36 @@ def batch_logpsi(params, cfg, xs):
     return torch.stack([logpsi(params, cfg, xs[b]) for b in range(xs.shape[0])])
 
 
+def logpsi_param_grad(params, cfg: OracleConfig, xs, ct):
+    """sum_b ct[b,0] dRe log psi_b/dp + ct[b,1] dIm log psi_b/dp by torch autograd: the
+    reference's jax.value_and_grad of network(params, x).real / .imag (loss.py:53-58)
+    contracted with the per-walker weights of loss_prod (loss.py:59-64)."""
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+    total = torch.zeros((), dtype=xs.dtype)
+    for b in range(xs.shape[0]):
+        lp = logpsi(P, cfg, xs[b])
+        total = total + float(ct[b][0]) * lp.real + float(ct[b][1]) * lp.imag
+    grads = torch.autograd.grad(total, list(P.values()), allow_unused=True)
+    return {k: (g if g is not None else torch.zeros_like(P[k])) for k, g in zip(P, grads)}
+
+
+def adam_reference(params, grads_seq, lr_fn, b1=0.9, b2=0.999, eps=1e-8):
+    """optax.adam (scale_by_adam + scale_by_learning_rate with a schedule), float64: the
+    update of optimizers/adam.py:24-43 applied for each gradient in ``grads_seq``."""
+    p = {k: v.clone() for k, v in params.items()}
+    mu = {k: torch.zeros_like(v) for k, v in p.items()}
+    nu = {k: torch.zeros_like(v) for k, v in p.items()}
+    for t, g in enumerate(grads_seq):
+        for k in p:
+            gk = torch.nan_to_num(g[k])
+            mu[k] = (1 - b1) * gk + b1 * mu[k]
+            nu[k] = (1 - b2) * gk * gk + b2 * nu[k]
+            mh = mu[k] / (1 - b1 ** (t + 1))
+            vh = nu[k] / (1 - b2 ** (t + 1))
+            p[k] = p[k] - lr_fn(t) * mh / (torch.sqrt(vh) + eps)
+    return p
+
+
 # --------------------------------------------------------------------------
 # MCMC (mcmc.py) with injected noise
 # --------------------------------------------------------------------------
@@ -453,10 +483,12 @@ def iqr_clip(x, scale=100.0):
     return iqr_clip_real(x.real, scale) + 1j * iqr_clip_real(x.imag, scale)
 
 
-def loss_stats(el, obs, ndev_means=None):
+def loss_stats(el, obs, ndev_means=None, penalties=False):
     """Device-local part of loss_and_grad stats (loss.py:66-92), single device.
 
     ``el`` complex [B]; ``obs`` dict of [B] arrays.  Returns dict of scalars.
+    ``penalties``: also the clipped Lz^2 / Lz / L^2 means of loss.py:79-80, 87 (needs the
+    angular-momentum keys in ``obs``).
     """
     el = np.asarray(el)
     out = {k: np.mean(np.asarray(v)) for k, v in obs.items()}
@@ -464,4 +496,22 @@ def loss_stats(el, obs, ndev_means=None):
     out["energy"] = energy
     out["clipped_energy"] = np.nanmean(iqr_clip(el))
     out["variance"] = np.nanmean(el.real**2) - energy.real**2
+    if penalties:
+        out["clipped_lz2"] = np.nanmean(iqr_clip(obs["angular_momentum_z_square"]))
+        out["clipped_lz"] = np.nanmean(iqr_clip(obs["angular_momentum_z"]))
+        out["clipped_l2"] = np.nanmean(iqr_clip(obs["angular_momentum_square"]))
     return out
+
+
+def loss_diff(el, obs, stats, lz_penalty=0.0, lz_center=0.0, l2_penalty=0.0):
+    """loss.py:75-89: diff = iqr_clip(E_L - <E_L>_clip + penalty terms); ``stats`` holds the
+    (device-averaged) clipped means of loss_stats(..., penalties=True)."""
+    d = np.asarray(el, dtype=np.complex128) - stats["clipped_energy"]
+    if lz_penalty:
+        lz2 = np.asarray(obs["angular_momentum_z_square"], dtype=np.float64)
+        lz = np.asarray(obs["angular_momentum_z"], dtype=np.float64)
+        d = d + lz_penalty * ((lz2 - stats["clipped_lz2"]) - 2 * lz_center * (lz - stats["clipped_lz"]))
+    if l2_penalty:
+        l2 = np.asarray(obs["angular_momentum_square"], dtype=np.float64)
+        d = d + l2_penalty * (l2 - stats["clipped_l2"])
+    return iqr_clip(d)

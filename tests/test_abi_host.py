@@ -16,7 +16,7 @@ import torch
 from deephall_amd import _lib
 from deephall_amd.config import Config, System
 from deephall_amd.mcmc import update_mcmc_width
-from deephall_amd.networks.psiformer import NetworkSpec, init_params, pack_params, param_shapes
+from deephall_amd.networks.psiformer import NetworkSpec, flat_params, init_params, param_shapes, ref_offsets
 from oracle import reference as R
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -83,34 +83,24 @@ def test_calls_without_params_fail_cleanly():
     lib.dh_destroy(h)
 
 
-def test_pack_params_layout_matches_reference_tree():
-    lib, spec, h, rc = make_handle(nspins=(2, 1), flux=3, num_heads=2, heads_dim=8, ndets=2)
-    nseg = lib.dh_param_layout(h, None, 0)
+@pytest.mark.parametrize("kw", [dict(), dict(nspins=(2, 1), flux=3, num_heads=2, heads_dim=8, ndets=2),
+                                dict(nspins=(20, 0), flux=57)])
+def test_ref_layout_matches_reference_tree(kw):
+    """dh_ref_layout (the flat reference tree the library packs on the device and the
+    gradient layout) == the Python ParamTree layout, in SURVEY.md Appendix B order."""
+    lib, spec, h, rc = make_handle(**kw)
+    assert rc == 0
+    nseg = lib.dh_ref_layout(h, None, 0)
+    nblk = 2 if spec.nspins[0] > 0 and spec.nspins[1] > 0 else 1
+    assert nseg == 1 + 15 * spec.num_layers + 4 * nblk + 2 == len(param_shapes(spec))
     offs = (C.c_size_t * (nseg + 1))()
-    lib.dh_param_layout(h, offs, nseg + 1)
-    offs = list(offs)
-    p = init_params(spec, seed=3)
-    buf = pack_params(spec, p, offs, "cpu").double()
-    D = spec.D
-    seg = lambda s, n: buf[offs[s] : offs[s] + n]  # noqa: E731
-    assert torch.allclose(seg(0, 4 * D), p["PsiformerLayers_0/Dense_0/kernel"].double().reshape(-1))
-    mha = "PsiformerLayers_0/MultiHeadAttention_0/"
-    wq = seg(1, D * 3 * D).reshape(D, 3 * D)
-    assert torch.allclose(wq[:, D : 2 * D], p[mha + "key/kernel"].double().reshape(D, D))
-    wol = seg(3, D * D).reshape(D, D)
-    ref = p[mha + "out/kernel"].double().reshape(D, D) @ p["PsiformerLayers_0/Dense_1/kernel"].double()
-    assert torch.allclose(wol, ref, atol=1e-6)
-    # orbital block order: (blk, part) = DenseGeneral_{2 blk + part}
-    L = spec.num_layers
-    MNK = spec.M * spec.nelec * spec.ndets
-    worb = buf[offs[1 + 8 * L] : offs[2 + 8 * L]][: D * ((4 * MNK + 127) // 128 * 128)].reshape(D, -1)
-    ob = "Orbitals_0/featured_orbitals/"
-    assert torch.allclose(worb[:, 3 * MNK : 4 * MNK], p[ob + "DenseGeneral_3/kernel"].double().reshape(D, MNK))
-    jas = buf[offs[3 + 8 * L] : offs[3 + 8 * L] + 2]
-    assert jas.tolist() == [1.0, 1.0]
-    w0qkv = buf[offs[4 + 8 * L] : offs[4 + 8 * L] + 4 * 3 * D].reshape(4, 3 * D)
-    wq0 = torch.cat([p[mha + n + "/kernel"].double().reshape(D, D) for n in ("query", "key", "value")], 1)
-    assert torch.allclose(w0qkv, p["PsiformerLayers_0/Dense_0/kernel"].double() @ wq0, atol=1e-6)
+    lib.dh_ref_layout(h, offs, nseg + 1)
+    assert list(offs) == ref_offsets(spec)
+    for (name, shape), a, b in zip(param_shapes(spec).items(), list(offs), list(offs)[1:]):
+        assert a % 64 == 0 and b - a >= int(np.prod(shape)), name
+    t = init_params(spec, seed=3)  # a ParamTree: views into one flat buffer
+    assert t.is_packed_view(spec) and t.flat.numel() == offs[nseg]
+    assert torch.equal(flat_params(spec, {k: v.clone() for k, v in t.items()}, "cpu"), t.flat)
     lib.dh_destroy(h)
 
 

@@ -243,31 +243,86 @@ def test_mcmc_sharding_invariance(cuda):
     assert torch.equal(xa, torch.cat([x0, x1]))
 
 
-@pytest.mark.parametrize("B", [1000, 4096, 20000])  # 20000: the one-part-at-a-time sort path
-def test_energy_stats_kernel(cuda, B):
-    ocfg = oracle_config("C1")
-    system, model = build(ocfg)
-    g = np.random.default_rng(B)
+def _stats_inputs(B, seed, ties=False):
+    g = np.random.default_rng(seed)
     e = g.standard_normal((B, 2)).astype(np.float32)
     e[:, 0] += 3.0
-    e[7, 0] = 1e6  # outlier gets clipped
-    e[9, 1] = np.nan  # NaN walker excluded from the nanmeans
+    if ties:  # heavy duplication: many equal keys in every radix digit
+        e = np.round(e * 4) / 4
     obs = g.standard_normal((B, 8)).astype(np.float32)
+    obs[:, 4] = np.abs(obs[:, 4]) * 3  # Lz^2 >= 0
+    if B > 9:
+        e[7, 0] = 1e6  # outlier gets clipped
+        e[9, 1] = np.nan  # NaN walker excluded from the nanmeans
+        obs[3, 5] = -5e4  # L^2 outlier
     nacc = g.integers(0, 11, B).astype(np.int32)
-    out = device_stats(model, torch.tensor(e, device=cuda), torch.tensor(obs, device=cuda),
-                       torch.tensor(nacc, device=cuda), steps=10).cpu().numpy()
-    el = np.empty(B, np.complex128)  # keep Re valid where only Im is NaN
+    return e, obs, nacc
+
+
+def _oracle_stats(e, obs):
+    el = np.empty(e.shape[0], np.complex128)  # keep Re valid where only Im is NaN
     el.real, el.imag = e[:, 0], e[:, 1]
-    o = {"kinetic": obs[:, 0] + 1j * obs[:, 1], "potential": obs[:, 2]}
-    ref = R.loss_stats(el, o)
-    assert out[0] == pytest.approx(ref["energy"].real, rel=1e-5)
-    assert out[1] == pytest.approx(ref["energy"].imag, abs=1e-5)
-    assert out[2] == pytest.approx(ref["clipped_energy"].real, rel=1e-5)
-    assert out[3] == pytest.approx(ref["clipped_energy"].imag, abs=1e-5)
-    assert out[4] == pytest.approx(np.nanmean(el.real**2), rel=1e-5)
-    assert out[5] == pytest.approx(obs[:, 0].mean(), abs=1e-5)
-    assert out[11] == pytest.approx(nacc.sum() / (10 * B), rel=1e-6)
-    assert out[12] == B - 1
+    o = {"kinetic": obs[:, 0] + 1j * obs[:, 1], "potential": obs[:, 2], "angular_momentum_z": obs[:, 3],
+         "angular_momentum_z_square": obs[:, 4], "angular_momentum_square": obs[:, 5]}
+    return el, o, R.loss_stats(el, o, penalties=True)
+
+
+@pytest.mark.parametrize("B,ties", [(1, False), (2, False), (7, True), (1000, False), (4096, True), (20000, False),
+                                    (40000, False), (131072, False)])
+def test_energy_stats_kernel(cuda, B, ties):
+    """dh_energy_stats against loss.py:30-38, 66-92 (oracle), every DH_STAT_* entry; any batch
+    size (radix-select quantiles), ties, NaN walkers, outliers; penalties on and off."""
+    ocfg = oracle_config("C1")
+    system, model = build(ocfg)
+    e, obs, nacc = _stats_inputs(B, B, ties)
+    el, o, ref = _oracle_stats(e, obs)
+    for pen in (False, True):
+        out = device_stats(model, torch.tensor(e, device=cuda), torch.tensor(obs, device=cuda),
+                           torch.tensor(nacc, device=cuda), steps=10, penalties=pen).cpu().numpy()
+        assert out[0] == pytest.approx(ref["energy"].real, rel=1e-5)
+        assert out[1] == pytest.approx(ref["energy"].imag, rel=1e-5, abs=1e-6)
+        assert out[2] == pytest.approx(ref["clipped_energy"].real, rel=1e-5)
+        assert out[3] == pytest.approx(ref["clipped_energy"].imag, rel=1e-5, abs=1e-6)
+        assert out[4] == pytest.approx(np.nanmean(el.real**2), rel=1e-5)
+        for i, k in ((5, "kinetic"), (7, "potential"), (8, "angular_momentum_z"), (9, "angular_momentum_z_square"),
+                     (10, "angular_momentum_square")):
+            want = ref[k].real
+            assert out[i] == pytest.approx(want, rel=1e-5, abs=1e-6), k
+        assert out[6] == pytest.approx(ref["kinetic"].imag, rel=1e-5, abs=1e-6)
+        assert out[11] == pytest.approx(nacc.sum() / (10 * B), rel=1e-6)
+        assert out[12] == np.sum(~(np.isnan(e[:, 0]) | np.isnan(e[:, 1])))
+        if pen:
+            for i, k in ((13, "clipped_lz2"), (14, "clipped_lz"), (15, "clipped_l2")):
+                assert out[i] == pytest.approx(ref[k].real, rel=1e-5, abs=1e-6), k
+        else:
+            assert (out[13:] == 0).all()
+
+
+@pytest.mark.parametrize("B", [1, 5, 4096, 50000])
+@pytest.mark.parametrize("pen", [(0.0, 0.0, 0.0), (0.3, 1.5, 0.2)])
+def test_loss_diff_kernel(cuda, B, pen):
+    """dh_loss_diff (clipped difference weighting the gradient) against loss.py:75-89."""
+    from deephall_amd.loss import loss_diff
+
+    ocfg = oracle_config("C1")
+    system, model = build(ocfg)
+    e, obs, _ = _stats_inputs(B, 100 + B)
+    el, o, ref = _oracle_stats(e, obs)
+    g = np.zeros(16, np.float32)
+    g[2], g[3] = ref["clipped_energy"].real, ref["clipped_energy"].imag
+    g[13], g[14], g[15] = ref["clipped_lz2"].real, ref["clipped_lz"].real, ref["clipped_l2"].real
+    diff, nvalid = loss_diff(model, torch.tensor(e, device=cuda), torch.tensor(obs, device=cuda),
+                             torch.tensor(g, device=cuda), *pen)
+    stats = {k: (np.complex64(v) if k == "clipped_energy" else np.float32(v)) for k, v in ref.items()
+             if k.startswith("clipped")}
+    want = R.loss_diff(el, o, stats, *pen)
+    got = diff.cpu().numpy()
+    nan_w = np.isnan(want.real) | np.isnan(want.imag)
+    assert np.array_equal(np.isnan(got[:, 0]) | np.isnan(got[:, 1]), nan_w)
+    scale = np.maximum(np.abs(want[~nan_w]), 1.0)
+    assert np.max(np.abs(got[~nan_w, 0] - want[~nan_w].real) / scale) < 2e-6
+    assert np.max(np.abs(got[~nan_w, 1] - want[~nan_w].imag) / scale) < 2e-6
+    assert float(nvalid) == np.sum(~nan_w)
 
 
 def test_walker_groups_on_parallel_streams_are_bit_identical(cuda):
