@@ -6,8 +6,9 @@ Public names mirror the reference package:
   local_energy           deephall.hamiltonian.local_energy   (alias make_local_energy)
   make_local_kinetic_energy, make_potential
   make_mcmc_step, update_mcmc_width   deephall.mcmc
-  make_loss_fn, LossMode              deephall.loss (energy statistics)
-  init_guess, initalize_state, setup_mcmc, vmc   deephall.train
+  make_loss_fn, LossMode              deephall.loss (statistics + parameter gradient)
+  make_optimizer_step                 deephall.optimizers (Adam, none)
+  train, init_guess, initalize_state, setup_mcmc, vmc   deephall.train
 All compute runs in the HIP library deephall_amd/_lib/libdeephall_amd.so.
 """
 
@@ -16,7 +17,9 @@ from .hamiltonian import local_energy, make_local_energy, make_local_kinetic_ene
 from .loss import LossMode, make_loss_fn
 from .mcmc import make_mcmc_step, update_mcmc_width
 from .networks import make_network
+from .optimizers import make_optimizer_step
 from .random import Key, PRNGKey
+from .train import train
 
 __all__ = [
     "Config",
@@ -38,4 +41,6 @@ __all__ = [
     "LossMode",
     "Key",
     "PRNGKey",
+    "make_optimizer_step",
+    "train",
 ]

@@ -1,14 +1,15 @@
-"""VMC inner loop driver — the hot-path callers of deephall/train.py.
-
-Reproduces, for the inference step (``optim.optimizer=none``,
-optimizers/none.py:22-35), the reference's setup and loop ordering:
+"""VMC driver — the callers of the hot path in deephall/train.py.
 
 * ``init_guess`` (train.py:40-54) — uniform walkers on the sphere, device RNG
 * ``initalize_state`` (train.py:57-65) — walkers sharded contiguously by rank
 * ``setup_mcmc`` (train.py:68-77)
-* ``vmc`` — burn-in (train.py:107-111), then per iteration: mcmc_step
-  (128-130), update_mcmc_width (131-137), energy statistics (140), log
-  (141-152), NaN abort (159-167).  One packed all-reduce per iteration.
+* ``train`` (train.py:80-167) — checkpoint restore or fresh state, burn-in, initial
+  energy, then per iteration: mcmc_step (128-130), update_mcmc_width (131-137), the
+  optimizer step (140: Adam or inference, optimizers.py), the stats row to
+  train_stats.csv (141-152), checkpoints by time/step interval, on NaN, at the last
+  step and on SIGINT/SIGTERM (154-165), NaN / signal abort (166-167)
+* ``vmc`` — the inference loop with the iteration's device work fused into one packed
+  statistics all-reduce (the bench's step)
 
 Multi-GPU: one process per GPU (torchrun-style env); each rank owns
 batch_size / world_size walkers.
@@ -18,6 +19,8 @@ from __future__ import annotations
 
 import logging
 import os
+import signal
+import time
 
 import numpy as np
 import torch
@@ -165,3 +168,96 @@ def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | Non
         if np.isnan(row["energy"].real):
             raise SystemExit("=" * 30 + " ABORT " + "=" * 30)
     return history
+
+
+class GracefulKiller:
+    """train.py:170-187: SIGINT / SIGTERM set a flag; the loop checkpoints and exits."""
+
+    kill_now = False
+
+    def __init__(self):
+        try:
+            signal.signal(signal.SIGINT, self.exit_gracefully)
+            signal.signal(signal.SIGTERM, self.exit_gracefully)
+        except ValueError:  # not the main thread
+            pass
+
+    def exit_gracefully(self, *args):
+        self.kill_now = True
+
+
+def train(cfg: Config):
+    """train.py:80-167 on MI355X.  Returns the final CheckpointState."""
+    from . import optimizers
+    from .config import OptimizerName
+    from .log import LogManager, init_logging
+    from .loss import LossMode, make_loss_fn
+    from .types import CheckpointState
+
+    init_logging()
+    init_distributed()
+    log_manager = LogManager(cfg)
+    model = make_network(cfg.system, cfg.network)
+    mcmc_step, pmoves = setup_mcmc(cfg, model)
+    opt_init, training_step = optimizers.make_optimizer_step(cfg, model)
+    key = PRNGKey(cfg.seed)
+    steps = cfg.mcmc.steps
+    device = torch.device("cuda", torch.cuda.current_device())
+    restored = log_manager.try_restore_checkpoint(model, device, opt_init)
+    if restored is not None:
+        initial_step, (params, data, opt_state, width) = restored
+        key = key.advance(steps * (cfg.mcmc.burn_in + initial_step))  # fresh draws after a restore
+    else:
+        initial_step, (params, data, opt_state, width) = initalize_state(cfg, model, device)
+    name = cfg.optim.optimizer
+    if (
+        name is not None and OptimizerName(getattr(name, "value", name)) == OptimizerName.none
+        and cfg.log.restore_path is not None and cfg.log.restore_path != cfg.log.save_path
+    ):  # inference after a training run starts its own step count (train.py:94-99)
+        initial_step = 0
+    if opt_state is None:
+        opt_state = opt_init(params, None, data)
+    logger.info("Start VMC with %s GPU process(es)", constants.world_size())
+    if initial_step == 0:
+        for _ in range(cfg.mcmc.burn_in):
+            data, _ = mcmc_step(params, data, key, width)
+            key = key.advance(steps)
+        logger.info("Burn in MCMC complete")
+        if cfg.log.initial_energy:
+            initial_stats, _ = make_loss_fn(model, cfg.system, LossMode.ENERGY_DIFF)(params, data)
+            logger.info("Initial energy: %s", float(initial_stats["energy"].real))
+    state = CheckpointState(params, data, opt_state, width)
+    last_save_time = time.time()
+    killer = GracefulKiller()
+    with log_manager.create_writer() as writer:
+        writer.hide("kinetic", "potential", "Lz_square")
+        for step in range(initial_step, cfg.optim.iterations):
+            new_data, pmove = mcmc_step(state.params, state.data, key, state.mcmc_width)
+            key = key.advance(steps)
+            new_width, pmoves = update_mcmc_width(step - initial_step, state.mcmc_width, cfg.mcmc.adapt_frequency,
+                                                  pmove, pmoves)
+            state = state._replace(data=new_data, mcmc_width=new_width)
+            state, stats = training_step(state, None)
+            energy = complex(stats["energy"].item())
+            writer.log(
+                step=str(step),
+                pmove=f"{float(pmove):.2f}",
+                energy=f"{energy.real:.4f}",
+                energy_imag=f"{energy.imag:+.4f}",
+                potential=f"{float(stats['potential']):.4f}",
+                kinetic=f"{complex(stats['kinetic'].item()).real:.4f}",
+                variance=f"{float(stats['variance']):.4f}",
+                Lz=f"{float(stats['angular_momentum_z']):+.4f}",
+                Lz_square=f"{float(stats['angular_momentum_z_square']):.4f}",
+                L_square=f"{float(stats['angular_momentum_square']):.4f}",
+            )
+            now = time.time()
+            nan = bool(np.isnan(energy.real))
+            if ((now - last_save_time > cfg.log.save_time_interval and (step + 1) % cfg.log.save_step_interval == 0)
+                    or nan or step == cfg.optim.iterations - 1 or killer.kill_now):
+                last_save_time = now
+                writer.force_flush()
+                log_manager.save_checkpoint(step, state)
+            if killer.kill_now or nan:
+                raise SystemExit("=" * 30 + " ABORT " + "=" * 30)
+    return state
