@@ -192,15 +192,15 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
   int* piv = reinterpret_cast<int*>(logdet + 1);
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const FView F{Fp, ldF, M, N, K};
-  float* cart = reinterpret_cast<float*>(piv + 2);  // [N][3] unit vectors
+  double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] unit vectors (double: close pairs)
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
     E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
   }
   for (int i = tid; i < N; i += nt) {
-    float st, ct, sp, cp;
-    sincosf(x[2 * (b * N + i)], &st, &ct);
-    sincosf(x[2 * (b * N + i) + 1], &sp, &cp);
+    double st, ct, sp, cp;
+    sincos((double)x[2 * (b * N + i)], &st, &ct);
+    sincos((double)x[2 * (b * N + i) + 1], &sp, &cp);
     cart[3 * i] = st * cp;
     cart[3 * i + 1] = st * sp;
     cart[3 * i + 2] = ct;
@@ -214,8 +214,8 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
     for (int q = tid; q < N * N; q += nt) {
       const int i = q / N, j = q - (q / N) * N;
       if (j <= i) continue;
-      const double dx = (double)cart[3 * j] - cart[3 * i], dy = (double)cart[3 * j + 1] - cart[3 * i + 1],
-                   dz = (double)cart[3 * j + 2] - cart[3 * i + 2];
+      const double dx = cart[3 * j] - cart[3 * i], dy = cart[3 * j + 1] - cart[3 * i + 1],
+                   dz = cart[3 * j + 2] - cart[3 * i + 2];
       const double r = sqrt(dx * dx + dy * dy + dz * dz);
       const bool same = (i < n_up) == (j < n_up);
       double f1, f2;
@@ -257,8 +257,8 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
 // ------------------------------------------------------------------ energy kernel
 struct DetSmem {
   int geo, alpha, E0, DTH, DPH, LB, D2TH, Aug, Binv, Phi, Mt, Mu, Gu, fac, ellt, ell0, ellL, ellS, red, misc;
-  int Fv, Fc, LB2, asmb, total;  // staged orbital rows (value, current channel); own-tangent LB terms;
-                                 // double-precision assembly partials
+  int Fv, Fc, LB2, asmb, dgeo, total;  // staged orbital rows (value, current channel); own-tangent LB
+                                       // terms; double-precision assembly partials; double geometry
 };
 // Orbital rows are staged through LDS when the N rows of one channel (the electron's own
 // spin block: 2 M N K floats each) fit this many floats.
@@ -278,6 +278,8 @@ __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
   o += 2 * NN;
   L.asmb = o;  // even offset: doubles
   o += 2 * (4 * T + 3 * N);
+  L.dgeo = o;  // even offset: (sin th, cos th, sin ph, cos ph) in double, from x
+  o += 2 * 4 * N;
   L.geo = o;
   o += 4 * N;
   L.alpha = o;
@@ -402,12 +404,23 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
     stage_store(Fv);
   }
 
+  // the double-precision parts (pair distances of the Jastrow and the potential, the
+  // assembly's geometry) take sin / cos of the walker coordinates in double: from f32
+  // sin / cos a close pair's chord sqrt(2 - 2 r_i . r_j) loses ~eps_f32 / r^2
+  double* dgeo = reinterpret_cast<double*>(sm + L.dgeo);
   for (int i = tid; i < N; i += nt) {
     const float4 g = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
     geo[4 * i] = g.x;
     geo[4 * i + 1] = g.y;
     geo[4 * i + 2] = g.z;
     geo[4 * i + 3] = g.w;
+    double st, ct, sp, cp;
+    sincos((double)x[2 * (b * N + i)], &st, &ct);
+    sincos((double)x[2 * (b * N + i) + 1], &sp, &cp);
+    dgeo[4 * i] = st;
+    dgeo[4 * i + 1] = ct;
+    dgeo[4 * i + 2] = sp;
+    dgeo[4 * i + 3] = cp;
   }
   __syncthreads();
   for (int t = tid; t < T; t += nt) {
@@ -642,13 +655,13 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
     lbr[t] = sr - (gr * gr - gi * gi);
     lbi[t] = si - 2.0 * gr * gi;
     // Jastrow gradient along the (scaled) tangent t of electron i
-    const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
+    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
     const double ri[3] = {sti * cpi, sti * spi, cti};
     const double et[3] = {(t & 1) ? -spi : cti * cpi, (t & 1) ? cpi : cti * spi, (t & 1) ? 0.0 : -sti};
     double jg = 0.0;
     for (int j = 0; j < N; ++j) {
       if (j == i) continue;
-      const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
+      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
       const double rj[3] = {stj * cpj, stj * spj, ctj};
       const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
       const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
@@ -658,16 +671,16 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
       jg += (-f1 / r) * (rj[0] * et[0] + rj[1] * et[1] + rj[2] * et[2]);
     }
     // gauge term A = i Q sum_i sigma_i phi_i (env_leaf) on the phi tangent
-    if (t & 1) gi += Q * ((cti >= 0.0) ? 1.0 : -1.0) / sti;
+    if (t & 1) gi += Q * ((geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0) / sti;  // the leaves' patch choice
     tgr[t] = gr + jg;
     tgi[t] = gi;
   } else if (tid < T + N) {
     const int i = tid - T;
-    const double sti = geo[4 * i], cti = geo[4 * i + 1], spi = geo[4 * i + 2], cpi = geo[4 * i + 3];
+    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
     const double ri[3] = {sti * cpi, sti * spi, cti};
     double J = 0.0, Jlb = 0.0, pe = 0.0;
     for (int j = i + 1; j < N; ++j) {
-      const double stj = geo[4 * j], ctj = geo[4 * j + 1], spj = geo[4 * j + 2], cpj = geo[4 * j + 3];
+      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
       const double rj[3] = {stj * cpj, stj * spj, ctj};
       const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
       const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
@@ -731,8 +744,8 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
     // gauge terms: phase and the flow channels' phi acceleration (see env_flow2)
     double gauge_phase = 0.0;
     for (int i = 0; i < N; ++i) {
-      const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
-      const double sg = (ct >= 0.0) ? 1.0 : -1.0;
+      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
+      const double sg = (geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0;  // the leaves' patch choice
       gauge_phase += Q * sg * (double)x[2 * (b * N + i) + 1];
       const double cot = ct / st;
       const double tdot[3] = {-sp, cp, 0.0};
@@ -751,7 +764,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
     }
     double Mv[3] = {0.0, 0.0, 0.0};
     for (int i = 0; i < N; ++i) {
-      const double st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
+      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
       const double cot = ct / st;
       mag_re += (Q * cot) * (Q * cot);
       mag_re += -2.0 * Q * cot * tgi[2 * i + 1];  // 2 i Q cot * t_phi_scaled
@@ -819,7 +832,7 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
   cf* logdet = ld + K;
   cf* wk = logdet + 1;                     // [K]
   int* piv = reinterpret_cast<int*>(wk + K);
-  float* cart = reinterpret_cast<float*>(piv + 2);  // [N][3]
+  double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] (double: close pairs)
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const FView F{Fp, ldF, M, N, K};
   const int MNK = M * N * K;
@@ -828,9 +841,9 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
     E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
   }
   for (int i = tid; i < N; i += nt) {
-    float st, ct_, sp, cp;
-    sincosf(x[2 * (b * N + i)], &st, &ct_);
-    sincosf(x[2 * (b * N + i) + 1], &sp, &cp);
+    double st, ct_, sp, cp;
+    sincos((double)x[2 * (b * N + i)], &st, &ct_);
+    sincos((double)x[2 * (b * N + i) + 1], &sp, &cp);
     cart[3 * i] = st * cp;
     cart[3 * i + 1] = st * sp;
     cart[3 * i + 2] = ct_;
@@ -851,8 +864,8 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
     for (int q = tid; q < N * N; q += nt) {
       const int i = q / N, j = q - (q / N) * N;
       if (j <= i) continue;
-      const double dx = (double)cart[3 * j] - cart[3 * i], dy = (double)cart[3 * j + 1] - cart[3 * i + 1],
-                   dz = (double)cart[3 * j + 2] - cart[3 * i + 2];
+      const double dx = cart[3 * j] - cart[3 * i], dy = cart[3 * j + 1] - cart[3 * i + 1],
+                   dz = cart[3 * j + 2] - cart[3 * i + 2];
       const double r = sqrt(dx * dx + dy * dy + dz * dz);
       const bool same = (i < n_up) == (j < n_up);
       const double al = same ? ap : aa, cst = same ? 0.25 : 0.5;
@@ -960,7 +973,7 @@ void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStrea
 
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s) {
-  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 3 * d.N) * sizeof(float);
+  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2) * sizeof(float);
   hipLaunchKernelGGL(det_value_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N,
                      d.n_up, d.M, d.K);
 }
@@ -968,7 +981,7 @@ void launch_det_value(const Dims& d, const float* F, const float* x, const float
 void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                     const float* ct, float* dF, float* jg, int nw, hipStream_t s) {
   const size_t bytes =
-      (size_t)(2 * d.N * d.M + 4 * d.N * d.N + 2 * d.N + 4 * d.K + 2 + 4 + 3 * d.N) * sizeof(float);
+      (size_t)(2 * d.N * d.M + 4 * d.N * d.N + 2 * d.N + 4 * d.K + 2 + 4 + 6 * d.N + 2) * sizeof(float);
   ensure_smem(det_bwd_kernel, bytes);
   hipLaunchKernelGGL(det_bwd_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, ct, dF, jg, d.N,
                      d.n_up, d.M, d.K, d.orb_cols);

@@ -2,7 +2,7 @@
 //
 //   propose_kernel  sph_sampling (mcmc.py:67-102): theta' = arctan(xi * width),
 //                   phi' = 2 pi U, rotate the pole onto each electron with
-//                   R_z(phi) R_y(theta), back to (theta, phi) with clipping.
+//                   R_z(phi) R_y(theta), back to (theta, phi) with clipping (double).
 //   accept_kernel   mh_update accept/select (mcmc.py:55-62): accept the whole
 //                   walker if 2 Re log psi(x') - lp > log U.
 //   init_kernel     init_guess (train.py:40-54): theta = arccos U(-1,1), phi = U(-pi,pi).
@@ -32,24 +32,29 @@ __global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ 
     xi = box_muller(r.x, r.y);
     up = u01(r.z);
   }
-  const float th = x[2 * e], ph = x[2 * e + 1];
-  const float thp = atanf(xi * width);
-  const float php = up * 2.f * kPi;
-  float stp, ctp, spp, cpp, st, ct, sp, cp;
-  sincosf(thp, &stp, &ctp);
-  sincosf(php, &spp, &cpp);
-  sincosf(th, &st, &ct);
-  sincosf(ph, &sp, &cp);
-  const float X = stp * cpp, Y = stp * spp, Z = ctp;
+  // The move is evaluated in double (the same formulas as mcmc.py:71-101, then rounded to
+  // f32): phi = sign(y) arccos(x / sin theta) loses ~eps / |sin phi| near phi = 0, pi in
+  // f32 (the reference's own f32 result is off by up to ~3e-4 rad there); in double the
+  // stored walker is the correctly rounded exact move.  ~20 double ops per electron.
+  const double th = x[2 * e], ph = x[2 * e + 1];
+  const double thp = atan((double)xi * (double)width);
+  const double php = (double)up * 2.0 * M_PI;
+  double stp, ctp, spp, cpp, st, ct, sp, cp;
+  sincos(thp, &stp, &ctp);
+  sincos(php, &spp, &cpp);
+  sincos(th, &st, &ct);
+  sincos(ph, &sp, &cp);
+  const double X = stp * cpp, Y = stp * spp, Z = ctp;
   // R_y(theta) then R_z(phi)
-  const float ax = ct * X + st * Z, ay = Y, az = -st * X + ct * Z;
-  const float x2x = cp * ax - sp * ay, x2y = sp * ax + cp * ay, x2z = az;
-  const float thn = acosf(fminf(fmaxf(x2z, -1.f), 1.f));
-  const float sgn = (x2y > 0.f) ? 1.f : ((x2y < 0.f) ? -1.f : 0.f);
-  const float q = x2x / sinf(thn);
+  const double ax = ct * X + st * Z, ay = Y, az = -st * X + ct * Z;
+  const double x2x = cp * ax - sp * ay, x2y = sp * ax + cp * ay, x2z = az;
+  const double thd = acos(fmin(fmax(x2z, -1.0), 1.0));
+  const double sgn = (x2y > 0.0) ? 1.0 : ((x2y < 0.0) ? -1.0 : 0.0);
+  const double q = x2x / sin(thd);
   // clip(q) with NaN propagation as jnp.clip (NaN in -> NaN out)
-  const float qc = (q != q) ? q : fminf(fmaxf(q, -1.f), 1.f);
-  const float phn = sgn * acosf(qc);
+  const double qc = (q != q) ? q : fmin(fmax(q, -1.0), 1.0);
+  const float thn = (float)thd;
+  const float phn = (float)(sgn * acos(qc));
   x2[2 * e] = thn;
   x2[2 * e + 1] = phn;
 }

@@ -51,6 +51,43 @@ def local_energy_case(name, B, seed=1898, param_seed=42):
     print("wrote", name, e.numpy()[:2])
 
 
+def pole_walkers(B, N, seed):
+    """init_guess walkers with electron 0 within 0.15 rad of the north pole and electron 1
+    within 0.15 rad of the south pole (theta in [1e-3, 0.15]): the cot / 1/sin^2 terms of
+    hamiltonian.py:121-159 are largest there, and the reference samples the poles freely."""
+    g = np.random.default_rng(seed)
+    x = R.init_guess_from_uniforms(g.random((B, N)), g.random((B, N)))
+    t = 10 ** g.uniform(-3, np.log10(0.15), size=(B, 2))
+    x[:, 0, 0] = t[:, 0]
+    if N > 1:
+        x[:, 1, 0] = np.pi - t[:, 1]
+    return x.astype(np.float32)
+
+
+def energy_case(tag, name, B, seed=1898, param_seed=42, pole=False, **over):
+    """Golden local energies with the float64 oracle AND the same full-Hessian algorithm run
+    in float32 (the reference's own arithmetic): the tests bound the kernels' error by the
+    error of that float32 run (the f32 floor) per observable."""
+    cfg = oracle_config(name, **over)
+    p = make_params(cfg, seed=param_seed)
+    x = pole_walkers(B, cfg.nelec, seed) if pole else make_walkers(B, cfg.nelec, seed=seed)
+    xt = torch.tensor(x, dtype=torch.float64)
+    lp = R.batch_logpsi(p, cfg, xt).numpy()
+    e, o = R.local_energy(p, cfg, xt)
+    p32 = {k: v.float() for k, v in p.items()}
+    x32 = torch.tensor(x, dtype=torch.float32)
+    lp32 = R.batch_logpsi(p32, cfg, x32).detach().numpy()
+    e32, o32 = R.local_energy(p32, cfg, x32)
+    out = dict(config=json.dumps(cfg.__dict__), param_seed=param_seed, x=x, logpsi=lp, e_l=e.detach().numpy(),
+               logpsi32=lp32, e_l32=e32.detach().numpy())
+    for key, k in (("kinetic", "kinetic"), ("potential", "potential"), ("lz", "angular_momentum_z"),
+                   ("lz2", "angular_momentum_z_square"), ("l2", "angular_momentum_square")):
+        out[key] = o[k].detach().numpy()
+        out[key + "32"] = o32[k].detach().numpy()
+    np.savez_compressed(HERE / f"energy_{tag}.npz", **out)
+    print("wrote", tag, e.detach().numpy()[:2])
+
+
 def mcmc_case(name, B=16, steps=4, width=0.3, seed=7):
     cfg = oracle_config(name)
     p = make_params(cfg)
@@ -87,10 +124,31 @@ def mcmc_case(name, B=16, steps=4, width=0.3, seed=7):
     print("wrote mcmc", name, n_acc)
 
 
-if __name__ == "__main__":
-    torch.set_num_threads(8)
+def round1():
     local_energy_case("C1", 8)
     local_energy_case("C2", 6)
     local_energy_case("MIX", 6)
     mcmc_case("C1")
     mcmc_case("C2", B=8, steps=3)
+
+
+def round2():
+    """Near-pole walkers, harmonic potential, explicit radius, C4 / C5 batches, each with
+    the float32 run of the same full-Hessian algorithm beside the float64 one."""
+    energy_case("C1_pole", "C1", 32, seed=31, pole=True)
+    energy_case("C2_pole", "C2", 16, seed=32, pole=True)
+    energy_case("MIX_pole", "MIX", 16, seed=33, pole=True)
+    energy_case("C1_harmonic", "C1", 16, seed=34, interaction_type="harmonic", interaction_strength=0.7)
+    energy_case("C2_harmonic_radius", "C2", 16, seed=35, interaction_type="harmonic", radius=2.5)
+    energy_case("C2_radius", "C2", 16, seed=36, radius=3.1)
+    energy_case("C2", "C2", 32, seed=37)
+    energy_case("C4", "C4", 32, seed=38)
+    energy_case("C5", "C5", 32, seed=39)
+    mcmc_case("C4", B=16, steps=3)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    # python make_golden.py [round1] [round2]   (default: both)
+    for part in sys.argv[1:] or ["round1", "round2"]:
+        {"round1": round1, "round2": round2}[part]()

@@ -84,3 +84,31 @@ def rel_err(a, b, floor=1.0):
     a = np.asarray(a)
     b = np.asarray(b)
     return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), floor)))
+
+
+def logpsi_f32_errors(p64, cfg, x):
+    """Per-walker relative error of Re log psi of the float32 run of the same forward pass
+    (the reference's arithmetic) on these walkers: the floor f32 kernels are held to."""
+    xt = torch.as_tensor(x, dtype=torch.float64)
+    ref = R.batch_logpsi(p64, cfg, xt).real.numpy()
+    got = R.batch_logpsi({k: v.float() for k, v in p64.items()}, cfg, xt.float()).real.detach().double().numpy()
+    return np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)
+
+
+FLOOR_X = 1.5        # median: at most 1.5x the float32 run's
+FLOOR_X_P90 = 2.0    # 90th percentile (the 3rd-4th worst of 32 walkers: conditioning-dominated)
+FLOOR_X_MAX = 6.0    # the single worst walker (an ill-conditioned orbital matrix dominates it)
+FLOOR_SLACK = 2e-7   # observables the float32 run happens to get (nearly) exact
+
+
+def within_f32_floor(err_hip, err_f32, floor_abs=0.0):
+    """The kernels' per-walker errors are at or below the float32 run's error distribution:
+    median within FLOOR_X, 90th percentile within FLOOR_X_P90 of the float32 run's, the
+    maximum within FLOOR_X_MAX, or everything below ``floor_abs`` (e.g. north_star's 1e-5)."""
+    e, f = np.asarray(err_hip, np.float64), np.asarray(err_f32, np.float64)
+    if e.max() <= floor_abs:
+        return True
+    ok = np.median(e) <= FLOOR_X * np.median(f) + FLOOR_SLACK
+    ok &= np.percentile(e, 90) <= FLOOR_X_P90 * np.percentile(f, 90) + FLOOR_SLACK
+    ok &= e.max() <= FLOOR_X_MAX * f.max() + FLOOR_SLACK
+    return bool(ok)

@@ -27,7 +27,7 @@ from deephall_amd.loss import device_stats
 from deephall_amd.mcmc import make_mcmc_step
 from deephall_amd.random import Key
 from deephall_amd.train import init_guess
-from helpers import cancellation_scales, make_params, make_walkers, oracle_config, rel_err, scaled_err, to_device_params
+from helpers import cancellation_scales, logpsi_f32_errors, make_params, make_walkers, oracle_config, rel_err, scaled_err, to_device_params, within_f32_floor
 from oracle import channels as CH
 from oracle import philox
 from oracle import reference as R
@@ -83,7 +83,8 @@ def test_golden_local_energy(cuda, name):
     params = to_device_params(p64)
     x = torch.tensor(g["x"], device=cuda)
     lp = model.apply(params, x).cpu().numpy()
-    assert rel_err(lp.real, g["logpsi"].real) < 2e-5
+    err = np.abs(lp.real - g["logpsi"].real) / np.maximum(np.abs(g["logpsi"].real), 1.0)
+    assert within_f32_floor(err, logpsi_f32_errors(p64, ocfg, g["x"]), 1e-5)
     assert phase_err(lp.imag, g["logpsi"].imag) < 1e-4
     e, o = hamiltonian.local_energy(model, system)(params, x)
     ref_o = {"kinetic": g["kinetic"], "potential": g["potential"], "angular_momentum_z": g["lz"],
@@ -106,7 +107,9 @@ def test_local_energy_vs_channel_oracle(cuda, name, B):
     ref_o["potential"] = pe
     check_energy(e, o, ke.numpy() + pe, ref_o, cancellation_scales(p64, ocfg, x))
     lp = model.apply(params, torch.tensor(x, device=cuda)).cpu().numpy()
-    assert rel_err(lp.real, lp_ref.numpy().real) < 2e-5
+    # 1e-5 relative, else within the float32 run's error distribution on these walkers
+    err = np.abs(lp.real - lp_ref.numpy().real) / np.maximum(np.abs(lp_ref.numpy().real), 1.0)
+    assert within_f32_floor(err, logpsi_f32_errors(p64, ocfg, x), 1e-5)
 
 
 @pytest.mark.parametrize("name", ["C1", "C2"])
@@ -175,7 +178,7 @@ def test_nan_and_edge_walkers_propagate(cuda):
     assert torch.equal(e1, e[:1])
 
 
-@pytest.mark.parametrize("name", ["C1", "C2"])
+@pytest.mark.parametrize("name", ["C1", "C2", "C4"])
 def test_golden_mcmc_injected_noise(cuda, name):
     g = np.load(GOLDEN / f"mcmc_{name}.npz")
     ocfg = R.OracleConfig(**json.loads(str(g["config"])))
@@ -188,9 +191,10 @@ def test_golden_mcmc_injected_noise(cuda, name):
     x = torch.tensor(g["x0"], device=cuda)
     x, pmove = step(params, x, Key(0), float(g["width"]), noise=noise)
     assert np.array_equal(step.last_n_accept.cpu().numpy(), g["n_acc"])
-    # phi = sign(y) arccos(x / sin th) (mcmc.py:101) is ill-conditioned at phi ~ 0, +-pi: the
-    # reference's own f32 evaluation is off by up to ~3e-4 there (tools/diag_proposal.py)
-    assert cart_err(x.cpu().numpy(), g["x"]) < 5e-4
+    # the proposal is evaluated in double on the device (mcmc.hip): positions are the
+    # float64 oracle's to f32 rounding (the reference's own f32 phi = sign(y) arccos(x /
+    # sin th), mcmc.py:101, is off by up to ~3e-4 near phi = 0, pi; tools/diag_proposal.py)
+    assert cart_err(x.cpu().numpy(), g["x"]) < 2e-6
     assert float(pmove) == pytest.approx(g["n_acc"].sum() / (steps * B))
     # lp must be 2 Re log psi of the walkers the device ended with
     lp_at_x = 2.0 * R.batch_logpsi(make_params(ocfg), ocfg, torch.tensor(x.cpu().numpy(), dtype=torch.float64)).real
@@ -347,3 +351,31 @@ def test_walker_groups_on_parallel_streams_are_bit_identical(cuda):
         else:
             for a, b in zip(ref, got):
                 assert torch.equal(a, b), groups
+
+
+def test_c3_global_batch_single_process(cuda):
+    """BASELINE.json configs[2]'s global batch (32768 walkers, N=6, 2Q=15) through one
+    process: MCMC, local energy (chunked by the workspace), statistics; rows are
+    independent of the batch they run in, the statistics equal numpy's on the same E_L."""
+    from deephall_amd.hamiltonian import _run_local_energy
+
+    ocfg = oracle_config("C2")
+    system, model = build(ocfg)
+    params = model.init(42, device=cuda)
+    B = 32768
+    x = init_guess(Key(5), B, ocfg.nelec, cuda, network=model)
+    step = make_mcmc_step(model, batch_per_device=B, steps=2)
+    x, pmove = step(params, x, Key(9), 0.1)
+    e, o = _run_local_energy(model, params, x)
+    e2, o2 = _run_local_energy(model, params, x[4096:8192].contiguous())
+    assert torch.equal(e[4096:8192], e2) and torch.equal(o[4096:8192], o2)
+    st = device_stats(model, e, o, step.last_n_accept, 2).cpu().numpy()
+    en, on = e.cpu().numpy().astype(np.float64), o.cpu().numpy().astype(np.float64)
+    assert np.isfinite(en).all()
+    el = en[:, 0] + 1j * en[:, 1]
+    ref = R.loss_stats(el, {"kinetic": on[:, 0] + 1j * on[:, 1], "angular_momentum_square": on[:, 5]})
+    assert st[0] == pytest.approx(ref["energy"].real, rel=1e-5)
+    assert st[2] == pytest.approx(ref["clipped_energy"].real, rel=1e-5)
+    assert st[5] == pytest.approx(ref["kinetic"].real, rel=1e-5)
+    assert st[10] == pytest.approx(ref["angular_momentum_square"], rel=1e-4, abs=1e-5)
+    assert st[11] == pytest.approx(float(pmove), rel=1e-6)
