@@ -149,7 +149,8 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
   if (cfg->num_layers < 0 || cfg->num_layers > 16) return fail(DH_EINVAL, "need num_layers <= 16");
   if (cfg->ndets < 1 || cfg->ndets > 16) return fail(DH_EINVAL, "need 1 <= determinants <= 16");
   if (cfg->num_heads < 1 || cfg->heads_dim < 1) return fail(DH_EINVAL, "bad attention shape");
-  if (cfg->orbital_type != DH_ORBITAL_FULL) return fail(DH_EINVAL, "only orbital type 'full' is supported");
+  if (cfg->orbital_type != DH_ORBITAL_FULL && cfg->orbital_type != DH_ORBITAL_SPARSE)
+    return fail(DH_EINVAL, "orbital type must be DH_ORBITAL_FULL or DH_ORBITAL_SPARSE");
   if (cfg->interaction_type != DH_INTERACTION_COULOMB && cfg->interaction_type != DH_INTERACTION_HARMONIC)
     return fail(DH_EINVAL, "bad interaction type");
   const int D = cfg->num_heads * cfg->heads_dim;
@@ -177,6 +178,7 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
   d.ld_orb = round_up(d.orb_cols, 128);
   d.interaction = cfg->interaction_type;
   d.lambda = cfg->interaction_strength;
+  d.sparse = cfg->orbital_type == DH_ORBITAL_SPARSE;
   // packed layout
   std::vector<size_t> sizes;
   sizes.push_back((size_t)4 * D);
@@ -202,7 +204,7 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
   h->offsets.push_back(off);
   // reference parameter tree, flattened in SURVEY.md Appendix B order (ref_seg below)
   {
-    const size_t DD = (size_t)D * D, MNK = (size_t)d.M * N * d.K;
+    const size_t DD = (size_t)D * D, FNK = (size_t)(d.sparse ? kSparseFeatures : d.M) * N * d.K;
     std::vector<size_t> rs;
     rs.push_back((size_t)4 * D);
     for (int l = 0; l < d.L; ++l)
@@ -210,8 +212,12 @@ int dh_create(const dh_config* cfg, dh_handle** out) {
                        (size_t)D, (size_t)D, (size_t)D})
         rs.push_back(v);
     for (int i = 0; i < 2 * d.NB; ++i) {
-      rs.push_back((size_t)D * MNK);
-      rs.push_back(MNK);
+      rs.push_back((size_t)D * FNK);
+      rs.push_back(FNK);
+    }
+    if (d.sparse) {  // Orbitals_0/lll_weight
+      rs.push_back((size_t)kSparseFeatures * d.M);
+      rs.push_back((size_t)d.M);
     }
     rs.push_back(1);
     rs.push_back(1);
@@ -263,12 +269,13 @@ namespace {
 
 // Reference-tree segment indices (dh_ref_layout)
 struct RefSeg {
-  int L, NB;
+  int L, NB, sparse;
   int W0() const { return 0; }
   int lay(int l, int k) const { return 1 + 15 * l + k; }  // k: Wq bq Wk bk Wv bv Wo bo Wl ln1s ln1b Wm bm ln2s ln2b
   int orb_kernel(int i) const { return 1 + 15 * L + 2 * i; }
   int orb_bias(int i) const { return 2 + 15 * L + 2 * i; }
-  int jas(int k) const { return 1 + 15 * L + 4 * NB + k; }
+  int lll(int k) const { return 1 + 15 * L + 4 * NB + k; }  // "sparse": lll_weight kernel, bias
+  int jas(int k) const { return 1 + 15 * L + 4 * NB + (sparse ? 2 : 0) + k; }
 };
 enum { RWq = 0, Rbq, RWk, Rbk, RWv, Rbv, RWo, Rbo, RWl, Rln1s, Rln1b, RWm, Rbm, Rln2s, Rln2b };
 
@@ -403,7 +410,7 @@ int ensure_param_buffers(dh_handle* h) {
 void pack_from_ref(dh_handle* h, hipStream_t st) {
   const Dims& d = h->d;
   const int D = d.D, MNK = d.M * d.N * d.K;
-  const RefSeg R{d.L, d.NB};
+  const RefSeg R{d.L, d.NB, d.sparse};
   auto ref = [&](int seg) { return h->ref + h->ref_offsets[seg]; };
   auto pk = [&](int seg) { return h->params + h->offsets[seg]; };
   launch_copy2d(ref(R.W0()), D, pk(0), D, 4, D, st);
@@ -426,8 +433,13 @@ void pack_from_ref(dh_handle* h, hipStream_t st) {
   launch_copy2d(nullptr, 0, pk(so), d.ld_orb, D, d.ld_orb, st);
   launch_copy2d(nullptr, 0, pk(so + 1), d.ld_orb, 1, d.ld_orb, st);
   for (int i = 0; i < 2 * d.NB; ++i) {
-    launch_copy2d(ref(R.orb_kernel(i)), MNK, pk(so) + i * MNK, d.ld_orb, D, MNK, st);
-    launch_copy2d(ref(R.orb_bias(i)), MNK, pk(so + 1) + i * MNK, d.ld_orb, 1, MNK, st);
+    if (d.sparse)  // fold lll_weight into the full layout (blocks.py:52-62)
+      launch_sparse_fold(ref(R.orb_kernel(i)), ref(R.orb_bias(i)), ref(R.lll(0)), ref(R.lll(1)), i % 2 == 0, D,
+                         d.N * d.K, d.M, pk(so) + i * MNK, d.ld_orb, pk(so + 1) + i * MNK, st);
+    else {
+      launch_copy2d(ref(R.orb_kernel(i)), MNK, pk(so) + i * MNK, d.ld_orb, D, MNK, st);
+      launch_copy2d(ref(R.orb_bias(i)), MNK, pk(so + 1) + i * MNK, d.ld_orb, 1, MNK, st);
+    }
   }
   launch_copy2d(ref(R.jas(0)), 1, pk(so + 2), 1, 1, 1, st);
   launch_copy2d(ref(R.jas(1)), 1, pk(so + 2) + 1, 1, 1, 1, st);
@@ -668,6 +680,7 @@ struct GradWork {
   float *hs[17], *qkv[16], *o[16], *t[16], *h1[16], *z[16];  // saved activations per layer
   float *dh, *dA, *dz, *dqkv, *dO;                            // backward temporaries
   float *P, *dWol, *dbol;                                     // chunk partials, folded-weight grads
+  float *dWorb, *dborb;                                       // full-layout orbital grads ("sparse")
   size_t total_bytes;
 };
 
@@ -706,6 +719,10 @@ GradWork carve_grad(const Dims& d, int nw, void* base) {
   w.P = take(std::max({nch * pw, nch * pc, (size_t)ln_bwd_blocks(rows) * 2 * D, (size_t)nw * 2}));
   w.dWol = take(D * D);
   w.dbol = take(D);
+  if (d.sparse) {
+    w.dWorb = take(D * d.ld_orb);
+    w.dborb = take(d.ld_orb);
+  }
   w.total_bytes = off * sizeof(float);
   return w;
 }
@@ -719,7 +736,7 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
   const Params& P = h->p;
   const int rows = nw * d.N, D = d.D, nch = grad_chunks(rows);
   const bool x6 = d.D % 32 == 0 && gemm_x6_supported(D);
-  const RefSeg RS{d.L, d.NB};
+  const RefSeg RS{d.L, d.NB, d.sparse};
   auto g = [&](int seg) { return grad + h->ref_offsets[seg]; };
   auto ref = [&](int seg) { return (const float*)h->ref + h->ref_offsets[seg]; };
   // forward GEMM Y = X W (+ bias) (+ R): the same arithmetic as the log-psi pass
@@ -777,10 +794,26 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
   {
     const int MNK = d.M * d.N * d.K;
     wgrad(w.hs[d.L], w.dF, d.ld_orb);
-    for (int i = 0; i < 2 * d.NB; ++i) wout(d.ld_orb, i * MNK, MNK, g(RS.orb_kernel(i)), MNK);
-    launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
-    for (int i = 0; i < 2 * d.NB; ++i)
-      launch_reduce2d(w.P + i * MNK, nch, (size_t)d.ld_orb, d.ld_orb, 1, MNK, g(RS.orb_bias(i)), MNK, 1.f, acc, s);
+    if (!d.sparse) {
+      for (int i = 0; i < 2 * d.NB; ++i) wout(d.ld_orb, i * MNK, MNK, g(RS.orb_kernel(i)), MNK);
+      launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
+      for (int i = 0; i < 2 * d.NB; ++i)
+        launch_reduce2d(w.P + i * MNK, nch, (size_t)d.ld_orb, d.ld_orb, 1, MNK, g(RS.orb_bias(i)), MNK, 1.f, acc, s);
+    } else {
+      // full-layout gradients of this chunk, then through the lll_weight fold
+      launch_reduce2d(w.P, nch, (size_t)D * d.ld_orb, d.ld_orb, D, d.orb_cols, w.dWorb, d.ld_orb, 1.f, 0, s);
+      launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
+      launch_reduce2d(w.P, nch, (size_t)d.ld_orb, d.ld_orb, 1, d.orb_cols, w.dborb, d.ld_orb, 1.f, 0, s);
+      SparseBlocks sb{};
+      sb.n = 2 * d.NB;
+      for (int i = 0; i < sb.n; ++i) {
+        sb.W8[i] = ref(RS.orb_kernel(i));
+        sb.b8[i] = ref(RS.orb_bias(i));
+        launch_sparse_unfold(w.dWorb + i * MNK, d.ld_orb, w.dborb + i * MNK, ref(RS.lll(0)), D, d.N * d.K, d.M,
+                             g(RS.orb_kernel(i)), g(RS.orb_bias(i)), acc, s);
+      }
+      launch_sparse_lll_grad(sb, w.dWorb, d.ld_orb, w.dborb, D, d.N * d.K, d.M, g(RS.lll(0)), g(RS.lll(1)), acc, s);
+    }
     bwd(w.dF, d.ld_orb, P.WorbB, P.WorbBT, nullptr, w.dh);
   }
   for (int l = d.L - 1; l >= 0; --l) {

@@ -22,7 +22,9 @@ struct Dims {
   int ld_orb;          // orb_cols rounded up to 128
   int interaction;     // DH_INTERACTION_*
   float lambda;        // interaction strength
+  int sparse;          // orbital type "sparse": F = 8 features per (j, k) (blocks.py:52-62)
 };
+constexpr int kSparseFeatures = 8;
 
 // Device pointers into the packed parameter buffer.
 struct LayerParams {
@@ -177,6 +179,26 @@ void launch_copy2d(const float* src, int lds, float* dst, int ldd, int nr, int n
 void launch_cotangent(const float* diff, const float* nvalid, int B, int part, float* ct, hipStream_t s);
 void launch_adam(float* p, const float* g, float* mu, float* nu, size_t n, float lr, float b1, float b2, float eps,
                  int step, hipStream_t s);
+// "sparse" orbitals (blocks.py:52-62): featured orbitals with 8 features per (j, k),
+// mixed into the M harmonics by lll_weight (DenseGeneral over axis 1, real kernel, bias on
+// the real part), folded into the full layout:
+//   Wfull[d][m NK + jk] = sum_a W8[d][a NK + jk] Wl[a][m]  (rows d < D; row D = the bias,
+//   with + bl[m] when `real_part`)
+void launch_sparse_fold(const float* W8, const float* b8, const float* Wl, const float* bl, int real_part, int D,
+                        int NK, int M, float* Wfull, int ldw, float* bfull, hipStream_t s);
+// gradient: dW8[d][a NK + jk] (+)= sum_m dWfull[d][m NK + jk] Wl[a][m] (rows d < D, row D bias)
+void launch_sparse_unfold(const float* dWfull, int ldw, const float* dbfull, const float* Wl, int D, int NK, int M,
+                          float* dW8, float* db8, int acc, hipStream_t s);
+// dWl[a][m] (+)= sum_{blocks i} [sum_d W8_i[d][a NK + jk] dWfull_i[d][m NK + jk] + b8_i . dbfull_i];
+// dbl[m] (+)= sum_{real blocks} sum_jk dbfull_i[m NK + jk].  W8s/b8s: per-block pointers.
+struct SparseBlocks {
+  const float* W8[4];
+  const float* b8[4];
+  int n;
+};
+void launch_sparse_lll_grad(SparseBlocks blk, const float* dWfull, int ldw, const float* dbfull, int D, int NK, int M,
+                            float* dWl, float* dbl, int acc, hipStream_t s);
+
 // det.hip: backward of log psi = J + log sum_k det Phi_k for per-walker cotangents ct[nw][2]:
 // dF [nw*N][ld_orb] (all columns written) and jg[nw][2] = ct.re * dJ / d(ee_par, ee_anti)
 void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,

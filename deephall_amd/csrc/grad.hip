@@ -402,6 +402,72 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   p[i] -= lr * (mh / (sqrtf(vh) + eps));
 }
 
+// ------------------------------------------------------------------ "sparse" orbitals
+__global__ __launch_bounds__(256) void sparse_fold_kernel(const float* __restrict__ W8, const float* __restrict__ b8,
+                                                          const float* __restrict__ Wl, const float* __restrict__ bl,
+                                                          int real_part, int D, int NK, int M, float* Wfull, int ldw,
+                                                          float* bfull) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t per = (size_t)M * NK;
+  if (i >= (size_t)(D + 1) * per) return;
+  const int d = (int)(i / per), rem = (int)(i % per), m = rem / NK, jk = rem % NK;
+  const float* src = d < D ? W8 + (size_t)d * kSparseFeatures * NK : b8;
+  double s = 0.0;
+#pragma unroll
+  for (int a = 0; a < kSparseFeatures; ++a) s += (double)src[a * NK + jk] * Wl[a * M + m];
+  if (d < D)
+    Wfull[(size_t)d * ldw + rem] = (float)s;
+  else
+    bfull[rem] = (float)(s + (real_part ? (double)bl[m] : 0.0));
+}
+
+__global__ __launch_bounds__(256) void sparse_unfold_kernel(const float* __restrict__ dWfull, int ldw,
+                                                            const float* __restrict__ dbfull,
+                                                            const float* __restrict__ Wl, int D, int NK, int M,
+                                                            float* dW8, float* db8, int acc) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t per = (size_t)kSparseFeatures * NK;
+  if (i >= (size_t)(D + 1) * per) return;
+  const int d = (int)(i / per), rem = (int)(i % per), a = rem / NK, jk = rem % NK;
+  const float* src = d < D ? dWfull + (size_t)d * ldw : dbfull;
+  double s = 0.0;
+  for (int m = 0; m < M; ++m) s += (double)src[m * NK + jk] * Wl[a * M + m];
+  float* o = d < D ? dW8 + (size_t)d * per + rem : db8 + rem;
+  *o = acc ? *o + (float)s : (float)s;
+}
+
+// one 256-thread block per (a, m) of lll_weight (+ M blocks for its bias)
+__global__ __launch_bounds__(256) void sparse_lll_grad_kernel(SparseBlocks blk, const float* __restrict__ dWfull,
+                                                              int ldw, const float* __restrict__ dbfull, int D, int NK,
+                                                              int M, float* dWl, float* dbl, int acc) {
+  __shared__ double red[4];
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int MNK = M * NK;
+  double s = 0.0;
+  if (o < kSparseFeatures * M) {
+    const int a = o / M, m = o % M;
+    for (int i = 0; i < blk.n; ++i)
+      for (int q = tid; q < (D + 1) * NK; q += 256) {
+        const int d = q / NK, jk = q % NK;
+        const float w8 = d < D ? blk.W8[i][(size_t)d * kSparseFeatures * NK + a * NK + jk] : blk.b8[i][a * NK + jk];
+        const float g = d < D ? dWfull[(size_t)d * ldw + i * MNK + m * NK + jk] : dbfull[i * MNK + m * NK + jk];
+        s += (double)w8 * g;
+      }
+  } else {
+    const int m = o - kSparseFeatures * M;
+    for (int i = 0; i < blk.n; i += 2)  // real-part blocks: (blk, part 0)
+      for (int jk = tid; jk < NK; jk += 256) s += dbfull[i * MNK + m * NK + jk];
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float v = (float)(red[0] + red[1] + red[2] + red[3]);
+    float* out = o < kSparseFeatures * M ? dWl + o : dbl + (o - kSparseFeatures * M);
+    *out = acc ? *out + v : v;
+  }
+}
+
 unsigned blocks_for(size_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
 
 }  // namespace
@@ -471,6 +537,24 @@ void launch_adam(float* p, const float* g, float* mu, float* nu, size_t n, float
                  int step, hipStream_t s) {
   const float bc1 = 1.f - powf(b1, (float)(step + 1)), bc2 = 1.f - powf(b2, (float)(step + 1));
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, s, p, g, mu, nu, n, lr, b1, b2, eps, bc1, bc2);
+}
+
+void launch_sparse_fold(const float* W8, const float* b8, const float* Wl, const float* bl, int real_part, int D,
+                        int NK, int M, float* Wfull, int ldw, float* bfull, hipStream_t s) {
+  hipLaunchKernelGGL(sparse_fold_kernel, dim3(blocks_for((size_t)(D + 1) * M * NK)), dim3(256), 0, s, W8, b8, Wl, bl,
+                     real_part, D, NK, M, Wfull, ldw, bfull);
+}
+
+void launch_sparse_unfold(const float* dWfull, int ldw, const float* dbfull, const float* Wl, int D, int NK, int M,
+                          float* dW8, float* db8, int acc, hipStream_t s) {
+  hipLaunchKernelGGL(sparse_unfold_kernel, dim3(blocks_for((size_t)(D + 1) * kSparseFeatures * NK)), dim3(256), 0, s,
+                     dWfull, ldw, dbfull, Wl, D, NK, M, dW8, db8, acc);
+}
+
+void launch_sparse_lll_grad(SparseBlocks blk, const float* dWfull, int ldw, const float* dbfull, int D, int NK, int M,
+                            float* dWl, float* dbl, int acc, hipStream_t s) {
+  hipLaunchKernelGGL(sparse_lll_grad_kernel, dim3(kSparseFeatures * M + M), dim3(256), 0, s, blk, dWfull, ldw, dbfull,
+                     D, NK, M, dWl, dbl, acc);
 }
 
 }  // namespace dh

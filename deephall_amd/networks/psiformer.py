@@ -76,7 +76,7 @@ class NetworkSpec:
         c.interaction_type = 0 if str(getattr(self.interaction_type, "value", self.interaction_type)) == "coulomb" else 1
         c.num_heads, c.heads_dim, c.num_layers = self.num_heads, self.heads_dim, self.num_layers
         c.ndets = self.ndets
-        c.orbital_type = 0 if str(getattr(self.orbital_type, "value", self.orbital_type)) == "full" else 1
+        c.orbital_type = {"full": 0, "sparse": 1}.get(str(getattr(self.orbital_type, "value", self.orbital_type)), -1)
         return c
 
 
@@ -200,9 +200,14 @@ def param_shapes(spec: NetworkSpec) -> dict:
         s[p + f"LayerNorm_{2 * l + 1}/bias"] = (D,)
     ob = "Orbitals_0/featured_orbitals/"
     nblk = sum(1 for n in spec.nspins if n > 0)
+    sparse = str(getattr(spec.orbital_type, "value", spec.orbital_type)) == "sparse"
+    F = 8 if sparse else M  # blocks.py:48-57
     for i in range(2 * nblk):
-        s[ob + f"DenseGeneral_{i}/kernel"] = (D, M, N, K)
-        s[ob + f"DenseGeneral_{i}/bias"] = (M, N, K)
+        s[ob + f"DenseGeneral_{i}/kernel"] = (D, F, N, K)
+        s[ob + f"DenseGeneral_{i}/bias"] = (F, N, K)
+    if sparse:  # lll_weight = DenseGeneral(2Q+1, axis=1), blocks.py:57
+        s["Orbitals_0/lll_weight/kernel"] = (8, M)
+        s["Orbitals_0/lll_weight/bias"] = (M,)
     s["Jastrow_0/ee_par"] = (1,)
     s["Jastrow_0/ee_anti"] = (1,)
     return s
@@ -305,8 +310,8 @@ class Psiformer:
         self.ndets = int(ndets)
         self.num_heads, self.heads_dim, self.num_layers = int(num_heads), int(heads_dim), int(num_layers)
         self.orbital_type = str(getattr(orbital_type, "value", orbital_type))
-        if self.orbital_type != "full":
-            raise NotImplementedError("orbital type 'sparse' (blocks.py:52-62) is not implemented on MI355X yet")
+        if self.orbital_type not in ("full", "sparse"):
+            raise ValueError(f"unknown orbital type {self.orbital_type!r}")
         radius = getattr(system, "radius", None) if system is not None else None
         lam = getattr(system, "interaction_strength", 1.0) if system is not None else 1.0
         itype = getattr(system, "interaction_type", "coulomb") if system is not None else "coulomb"

@@ -53,7 +53,8 @@ extern "C" {
 #define DH_INTERACTION_COULOMB 0
 #define DH_INTERACTION_HARMONIC 1
 #define DH_ORBITAL_FULL 0
-#define DH_ORBITAL_SPARSE 1 /* not supported yet: dh_create returns DH_EINVAL */
+#define DH_ORBITAL_SPARSE 1 /* blocks.py:52-62: 8 features per (j, k) mixed into the M harmonics by
+                               lll_weight; folded into the full layout when parameters are set */
 
 /* System + Network fields of deephall/config.py:56-104 that the hot path reads. */
 typedef struct dh_config {
@@ -110,8 +111,9 @@ int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream)
  *     MultiHeadAttention_l/out/{kernel [H*dh][D], bias [D]}                   (+6, +7)
  *     Dense_{2l+1}/kernel [D][D]; LayerNorm_{2l}/{scale, bias} [D]             (+8..+10)
  *     Dense_{2l+2}/{kernel [D][D], bias [D]}; LayerNorm_{2l+1}/{scale, bias}   (+11..+14)
- *   1+15L+2i, +1      Orbitals_0/featured_orbitals/DenseGeneral_i/{kernel [D][M*N*K],
- *                     bias [M*N*K]}, i < 2 * (spin blocks)
+ *   1+15L+2i, +1      Orbitals_0/featured_orbitals/DenseGeneral_i/{kernel [D][F*N*K],
+ *                     bias [F*N*K]}, i < 2 * (spin blocks); F = M ("full") or 8 ("sparse")
+ *   "sparse" only:    Orbitals_0/lll_weight/{kernel [8][M], bias [M]}
  *   then              Jastrow_0/ee_par [1], Jastrow_0/ee_anti [1]
  * Segments are 64-float aligned.  Returns the segment count; offsets[nseg] = total floats.
  * Parameter gradients (dh_logpsi_vjp) use the same layout. */

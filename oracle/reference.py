@@ -44,6 +44,7 @@ class OracleConfig:
     heads_dim: int = 64
     num_layers: int = 2
     determinants: int = 1
+    orbital: str = "full"
 
     @property
     def nelec(self):
@@ -85,12 +86,16 @@ def param_shapes(cfg: OracleConfig) -> dict:
         shapes[p + f"LayerNorm_{2 * l + 1}/scale"] = (D,)
         shapes[p + f"LayerNorm_{2 * l + 1}/bias"] = (D,)
     ob = "Orbitals_0/featured_orbitals/"
-    nblocks = 2 if cfg.nspins[1] > 0 else 1
+    nblocks = 2 if cfg.nspins[1] > 0 and cfg.nspins[0] > 0 else 1
+    F = 8 if cfg.orbital == "sparse" else M  # blocks.py:48-57
     for blk in range(nblocks):
         for part in range(2):  # real, imag  (blocks.py:30-31)
             idx = 2 * blk + part
-            shapes[ob + f"DenseGeneral_{idx}/kernel"] = (D, M, N, K)
-            shapes[ob + f"DenseGeneral_{idx}/bias"] = (M, N, K)
+            shapes[ob + f"DenseGeneral_{idx}/kernel"] = (D, F, N, K)
+            shapes[ob + f"DenseGeneral_{idx}/bias"] = (F, N, K)
+    if cfg.orbital == "sparse":  # lll_weight = DenseGeneral(2Q+1, axis=1) (blocks.py:57)
+        shapes["Orbitals_0/lll_weight/kernel"] = (8, M)
+        shapes["Orbitals_0/lll_weight/bias"] = (M,)
     shapes["Jastrow_0/ee_par"] = (1,)
     shapes["Jastrow_0/ee_anti"] = (1,)
     return shapes
@@ -200,7 +205,13 @@ def orbitals(params, cfg: OracleConfig, x):
         ]
         blocks.append(torch.complex(re, im))
         blk += 1
-    F = torch.cat(blocks, 0)  # [N, M, N, K]
+    F = torch.cat(blocks, 0)  # [N, M, N, K]  ("sparse": [N, 8, N, K])
+    if cfg.orbital == "sparse":
+        # lll_weight: DenseGeneral over axis 1 (real kernel [8, M], real bias added to the complex
+        # value), output moved to axis 1 (blocks.py:61-62)
+        W = params["Orbitals_0/lll_weight/kernel"].to(F.real.dtype)
+        b = params["Orbitals_0/lll_weight/bias"].to(F.real.dtype)
+        F = torch.einsum("najk,am->nmjk", F, W.to(F.dtype)) + b[None, :, None, None]
     env = envelope(cfg, theta, phi)  # [N, M]
     orb = (F * env[:, :, None, None]).sum(1)  # [N, N, K]
     orb = orb.permute(2, 0, 1)  # [K, N, N]

@@ -66,7 +66,7 @@ def test_create_layout_workspace():
 
 @pytest.mark.parametrize(
     "bad",
-    [dict(nspins=(0, 0)), dict(nspins=(40, 0)), dict(ndets=0), dict(ndets=17), dict(orbital_type="sparse"),
+    [dict(nspins=(0, 0)), dict(nspins=(40, 0)), dict(ndets=0), dict(ndets=17), dict(orbital_type="bogus"),
      dict(num_heads=1, heads_dim=3)],
 )
 def test_create_rejects_bad_configs(bad):
@@ -84,7 +84,8 @@ def test_calls_without_params_fail_cleanly():
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(nspins=(2, 1), flux=3, num_heads=2, heads_dim=8, ndets=2),
-                                dict(nspins=(20, 0), flux=57)])
+                                dict(nspins=(20, 0), flux=57), dict(orbital_type="sparse"),
+                                dict(nspins=(2, 2), flux=5, orbital_type="sparse")])
 def test_ref_layout_matches_reference_tree(kw):
     """dh_ref_layout (the flat reference tree the library packs on the device and the
     gradient layout) == the Python ParamTree layout, in SURVEY.md Appendix B order."""
@@ -92,7 +93,8 @@ def test_ref_layout_matches_reference_tree(kw):
     assert rc == 0
     nseg = lib.dh_ref_layout(h, None, 0)
     nblk = 2 if spec.nspins[0] > 0 and spec.nspins[1] > 0 else 1
-    assert nseg == 1 + 15 * spec.num_layers + 4 * nblk + 2 == len(param_shapes(spec))
+    lll = 2 if spec.orbital_type == "sparse" else 0
+    assert nseg == 1 + 15 * spec.num_layers + 4 * nblk + lll + 2 == len(param_shapes(spec))
     offs = (C.c_size_t * (nseg + 1))()
     lib.dh_ref_layout(h, offs, nseg + 1)
     assert list(offs) == ref_offsets(spec)
@@ -104,10 +106,12 @@ def test_ref_layout_matches_reference_tree(kw):
     lib.dh_destroy(h)
 
 
-def test_param_tree_matches_oracle_names():
-    spec = NetworkSpec(nspins=(3, 0), flux=2, ndets=1, num_heads=4, heads_dim=64, num_layers=2)
-    ocfg = R.OracleConfig(nspins=(3, 0), flux=2)
-    assert set(param_shapes(spec)) == set(R.param_shapes(ocfg))
+@pytest.mark.parametrize("orbital", ["full", "sparse"])
+@pytest.mark.parametrize("nspins", [(3, 0), (2, 2)])
+def test_param_tree_matches_oracle_names(orbital, nspins):
+    spec = NetworkSpec(nspins=nspins, flux=2, ndets=1, num_heads=4, heads_dim=64, num_layers=2, orbital_type=orbital)
+    ocfg = R.OracleConfig(nspins=nspins, flux=2, orbital=orbital)
+    assert list(param_shapes(spec)) == list(R.param_shapes(ocfg))  # same names, same order
     for k, v in R.param_shapes(ocfg).items():
         assert tuple(param_shapes(spec)[k]) == tuple(v)
 

@@ -38,9 +38,10 @@ def grad_errors(g_dev, g_ref, floor=1e-3):
     return errs
 
 
-@pytest.mark.parametrize("name,B", [("C1", 8), ("C2", 6), ("MIX", 8)])
-def test_vjp_matches_autograd(cuda, name, B):
-    ocfg = oracle_config(name)
+@pytest.mark.parametrize("name,B,orbital", [("C1", 8, "full"), ("C2", 6, "full"), ("MIX", 8, "full"),
+                                            ("C1", 6, "sparse"), ("MIX", 6, "sparse")])
+def test_vjp_matches_autograd(cuda, name, B, orbital):
+    ocfg = oracle_config(name, orbital=orbital)
     p64 = make_params(ocfg)
     system, model = build(ocfg)
     params = to_device_params(p64)

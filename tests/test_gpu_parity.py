@@ -46,6 +46,7 @@ def build(ocfg):
     net = config.Network()
     net.psiformer.num_heads, net.psiformer.heads_dim = ocfg.num_heads, ocfg.heads_dim
     net.psiformer.num_layers, net.psiformer.determinants = ocfg.num_layers, ocfg.determinants
+    net.orbital = config.OrbitalType(getattr(ocfg, "orbital", "full"))
     return system, make_network(system, net)
 
 
@@ -379,3 +380,33 @@ def test_c3_global_batch_single_process(cuda):
     assert st[5] == pytest.approx(ref["kinetic"].real, rel=1e-5)
     assert st[10] == pytest.approx(ref["angular_momentum_square"], rel=1e-4, abs=1e-5)
     assert st[11] == pytest.approx(float(pmove), rel=1e-6)
+
+
+@pytest.mark.parametrize("name,B", [("C1", 6), ("MIX", 6), ("C2", 4)])
+def test_sparse_orbitals_vs_oracle(cuda, name, B):
+    """Orbital type "sparse" (blocks.py:52-62): 8 featured orbitals mixed into the 2Q+1
+    harmonics by lll_weight, folded into the full layout on the device; log psi and the
+    local energy against the float64 full-Hessian restatement."""
+    ocfg = oracle_config(name, orbital="sparse")
+    p64 = make_params(ocfg)
+    system, model = build(ocfg)
+    params = to_device_params(p64)
+    x = make_walkers(B, ocfg.nelec, seed=13)
+    xt = torch.tensor(x, dtype=torch.float64)
+    lp_ref = R.batch_logpsi(p64, ocfg, xt).numpy()
+    lp = model.apply(params, torch.tensor(x, device=cuda)).cpu().numpy()
+    err = np.abs(lp.real - lp_ref.real) / np.maximum(np.abs(lp_ref.real), 1.0)
+    assert within_f32_floor(err, logpsi_f32_errors(p64, ocfg, x), 1e-5)
+    assert phase_err(lp.imag, lp_ref.imag) < 1e-4
+    e_ref, o_ref = R.local_energy(p64, ocfg, xt)
+    e32, o32 = R.local_energy({k: v.float() for k, v in p64.items()}, ocfg, xt.float())
+    e, o = hamiltonian.local_energy(model, system)(params, torch.tensor(x, device=cuda))
+    o = dict(o, e_l=e)
+    o_ref = dict(o_ref, e_l=e_ref)
+    o32 = dict(o32, e_l=e32)
+    for k in ("e_l", "kinetic", "potential", "angular_momentum_z", "angular_momentum_z_square",
+              "angular_momentum_square"):
+        ref = o_ref[k].detach().numpy()
+        eh = np.abs(o[k].cpu().numpy() - ref) / np.maximum(np.abs(ref), 1.0)
+        e3 = np.abs(o32[k].detach().double().numpy() - ref) / np.maximum(np.abs(ref), 1.0)
+        assert within_f32_floor(eh, e3, 1e-5), (k, eh.max(), e3.max())
