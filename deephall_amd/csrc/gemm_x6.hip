@@ -596,7 +596,8 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   constexpr int A_BYTES = BM * BK * 4, B_PLANE = BN * BK * 2, STAGE = A_BYTES + 3 * B_PLANE;
   constexpr int IA = A_BYTES / 1024, IB = (3 * B_PLANE) / 1024, PER = (IA + IB + NWT - 1) / NWT;
   static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
-  static_assert(ST == 2 || ST == 3, "ring depth");
+  static_assert(ST >= 2 && ST <= 6, "ring depth");
+  static_assert(ST <= 3 || (ST - 3) * PER <= 63, "vmcnt range");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -697,10 +698,13 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
       __syncthreads();                                  // ... and buffer cur is free
     }
   } else {
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  if (nk > 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  // ring of ST buffers, ST - 2 stages in flight while a k-tile computes: stages 0 .. ST-2
+  // issued up front; at k-tile kt, wait for stage kt + 1 (the younger ST - 3 may stay in
+  // flight: VMEM ops of a wave complete in order), barrier, issue stage kt + ST - 1 into the
+  // buffer k-tile kt - 1 used
+  for (int t = 0; t < ST - 1 && t < nk; ++t) stage(t, t);
+  if (nk > ST - 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((ST - 2) * PER) : "memory");
   else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -714,13 +718,16 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   bf16x8 rb0 = c0, rb1 = c1, rb2 = c2;  // ABL 3 operands
   for (int kt = 0; kt < nk; ++kt) {
     if (ABL == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued one iteration ago)
+      if (ST > 3 && kt + ST - 2 < nk)  // stages kt + 2 .. kt + ST - 2 issued: they may stay in flight
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((ST > 3 ? ST - 3 : 0) * PER) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage kt+1 (issued earlier)
       __syncthreads();
     }
-    int bn1 = bcur + 1, bn2 = bcur + 2;
-    if (bn1 >= 3) bn1 -= 3;
-    if (bn2 >= 3) bn2 -= 3;
-    if (ABL == 0 && kt + 2 < nk) stage(kt + 2, bn2);
+    int bn1 = bcur + 1, bnl = bcur + ST - 1;
+    if (bn1 >= ST) bn1 -= ST;
+    if (bnl >= ST) bnl -= ST;
+    if (ABL == 0 && kt + ST - 1 < nk) stage(kt + ST - 1, bnl);
     const bool more = kt + 1 < nk;
     float4 u, v;
     if (more) {
@@ -1522,6 +1529,28 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
     case 62:
       launch_x6d_t<2, 0, 4, 3, 0, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
+    // deeper rings (ST - 2 stages in flight): 96 x 256 of 3 x 4 waves, 128 x 192 / 256 x 128
+    case 70:
+      if (round_up(rows, 96) <= round_up(rows, 256)) {
+        launch_x6d_t<2, 0, 3, 5, 0, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+        break;
+      }
+      [[fallthrough]];
+    case 71:
+      launch_x6d_t<6, 0, 4, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 72:
+      launch_x6d_t<6, 0, 4, 5>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 73:
+      launch_x6d_t<4, 0, 8, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 74:
+      launch_x6d_t<8, 0, 4, 4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 75:
+      launch_x6d_t<4, 0, 4, 5>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
     // persistent lean
     case 50:
       launch_x6q_t<8>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
@@ -1576,7 +1605,14 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat) {
   if (mode != 0) feat = X6Feat{};
   const bool r96 = round_up(rows, 96) <= round_up(rows, 256);
-  if (nw < 1 || nw > 4 || (!r96 && (nw == 1 || nw == 3))) nw = r96 ? 1 : 2;
+  if (nw < 1 || nw > 7 || (!r96 && (nw == 1 || nw == 3 || nw == 5 || nw == 6))) nw = r96 ? 1 : 2;
+#define DH_X6LN_ST(TNV, NWV, WNV, STV)                                                                      \
+  do {                                                                                                      \
+    if (mode == 0)                                                                                          \
+      launch_x6d_t<TNV, 0, NWV, STV, 1, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln, feat); \
+    else                                                                                                    \
+      launch_x6d_t<TNV, 0, NWV, STV, 2, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln); \
+  } while (0)
 #define DH_X6LN(TNV, NWV, WNV)                                                                              \
   do {                                                                                                      \
     if (mode == 0)                                                                                          \
@@ -1588,9 +1624,13 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
     case 1: DH_X6LN(2, 3, 4); break;
     case 2: DH_X6LN(2, 2, 4); break;
     case 3: DH_X6LN(8, 3, 1); break;
+    case 5: DH_X6LN_ST(2, 3, 4, 5); break;
+    case 6: DH_X6LN_ST(2, 3, 4, 4); break;
+    case 7: DH_X6LN_ST(2, 2, 4, 5); break;
     default: DH_X6LN(8, 4, 1);
   }
 #undef DH_X6LN
+#undef DH_X6LN_ST
 }
 
 }  // namespace dh
