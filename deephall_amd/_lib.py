@@ -83,6 +83,9 @@ class DhConfig(C.Structure):
         ("num_layers", C.c_int),
         ("ndets", C.c_int),
         ("orbital_type", C.c_int),
+        ("network_type", C.c_int),
+        ("excitation_lz", C.c_float),
+        ("cf_flux", C.c_int),
     ]
 
 

@@ -106,6 +106,9 @@ struct dh_handle {
   std::vector<float> norm_host;
   bool params_set = false;
   bool ref_set = false;
+  bool laughlin = false;          // DH_NETWORK_LAUGHLIN: no parameters, laughlin.hip kernels
+  std::vector<int> expo_host;     // Laughlin exponents [2][N] = (Q1 + m_j, Q1 - m_j)
+  int* expo = nullptr;            // device copy (uploaded at first use)
   Profiler prof;
 };
 
@@ -141,8 +144,80 @@ extern "C" {
 const char* dh_last_error(void) { return g_err.c_str(); }
 const char* dh_version(void) { return "deephall_amd 0.1 (gfx950)"; }
 
+namespace {
+// Laughlin(nspins, flux, cf_flux, excitation_lz) (laughlin.py:19-46): exponents of the
+// composite-fermion orbitals, in doubled units (2 Q1, 2 m are integers)
+int laughlin_exponents(const dh_config* cfg, std::vector<int>& ex) {
+  const int N = cfg->n_up + cfg->n_dn;
+  const int p = cfg->cf_flux < 1 ? 1 : cfg->cf_flux;
+  const int q2 = cfg->flux - 2 * p * (N - 1);  // 2 Q1
+  if (q2 < 0) return fail(DH_EINVAL, "Laughlin: flux too small for N electrons (Q1 < 0)");
+  std::vector<int> m2;  // 2 m
+  if (N == q2 + 1) {  // ground state
+    for (int m = -q2; m <= q2; m += 2) m2.push_back(m);
+  } else if (N == q2) {  // quasihole: m = -Q1 .. Q1 without -lz (laughlin.py:66-73)
+    const double lz2 = 2.0 * cfg->excitation_lz;
+    const int l2 = (int)std::lround(lz2);
+    if (std::fabs(lz2 - l2) > 1e-6 || ((l2 - q2) % 2) != 0 || std::abs(l2) > q2)
+      return fail(DH_EINVAL, "Laughlin quasihole: impossible excitation_lz");
+    for (int m = -q2; m < -l2; m += 2) m2.push_back(m);
+    for (int m = q2; m > -l2; m -= 2) m2.push_back(m);
+  } else if (N == q2 + 2) {
+    return fail(DH_EINVAL, "Laughlin quasiparticle states (laughlin.py:82-100) are not supported on MI355X yet");
+  } else {
+    return fail(DH_EINVAL, "Laughlin: filling not supported");
+  }
+  if ((int)m2.size() != N) return fail(DH_EINVAL, "Laughlin: orbital count mismatch");
+  ex.assign(2 * N, 0);
+  for (int j = 0; j < N; ++j) {
+    ex[j] = (q2 + m2[j]) / 2;
+    ex[N + j] = (q2 - m2[j]) / 2;
+  }
+  return DH_OK;
+}
+}  // namespace
+
 int dh_create(const dh_config* cfg, dh_handle** out) {
   if (!cfg || !out) return fail(DH_EINVAL, "null argument");
+  if (cfg->network_type == DH_NETWORK_LAUGHLIN) {
+    const int N = cfg->n_up + cfg->n_dn;
+    if (cfg->n_up < 0 || cfg->n_dn < 0 || N < 1 || N > 32) return fail(DH_EINVAL, "need 1 <= N <= 32 electrons");
+    if (cfg->flux < 1 || cfg->flux > 126) return fail(DH_EINVAL, "Laughlin needs 1 <= flux <= 126");
+    if (cfg->interaction_type != DH_INTERACTION_COULOMB && cfg->interaction_type != DH_INTERACTION_HARMONIC)
+      return fail(DH_EINVAL, "bad interaction type");
+    std::vector<int> ex;
+    if (int rc = laughlin_exponents(cfg, ex)) return rc;
+    auto* h = new dh_handle();
+    h->cfg = *cfg;
+    h->laughlin = true;
+    h->expo_host = ex;
+    Dims& d = h->d;
+    d = Dims{};
+    d.N = N;
+    d.n_up = cfg->n_up;
+    d.n_dn = cfg->n_dn;
+    d.T = 2 * N;
+    d.C = 2 * N + 5;
+    d.M = 1;
+    d.Q = 0.5f * cfg->flux;
+    d.r = cfg->radius > 0.f ? cfg->radius : std::sqrt(d.Q);
+    d.H = 1;
+    d.dh = 4;
+    d.D = 4;
+    d.L = 0;
+    d.K = 1;
+    d.NB = 1;
+    d.orb_cols = 0;
+    d.ld_orb = 0;
+    d.interaction = cfg->interaction_type;
+    d.lambda = cfg->interaction_strength;
+    h->offsets = {0};
+    h->ref_offsets = {0};
+    h->params_set = h->ref_set = true;  // nothing to upload
+    *out = h;
+    return DH_OK;
+  }
+  if (cfg->network_type != DH_NETWORK_PSIFORMER) return fail(DH_EINVAL, "bad network type");
   const int N = cfg->n_up + cfg->n_dn;
   if (cfg->n_up < 0 || cfg->n_dn < 0 || N < 1 || N > 32) return fail(DH_EINVAL, "need 1 <= N <= 32 electrons");
   if (cfg->flux < 0 || cfg->flux > 126) return fail(DH_EINVAL, "need 0 <= flux <= 126");
@@ -253,6 +328,7 @@ void dh_destroy(dh_handle* h) {
   if (h->ref) (void)hipFree(h->ref);
   if (h->wb) (void)hipFree(h->wb);
   if (h->wbt) (void)hipFree(h->wbt);
+  if (h->expo) (void)hipFree(h->expo);
   delete h;
 }
 
@@ -451,6 +527,7 @@ void pack_from_ref(dh_handle* h, hipStream_t st) {
 extern "C" {
 
 int dh_set_params(dh_handle* h, const float* params, size_t count, void* stream) {
+  if (h && h->laughlin) return count == 0 ? DH_OK : fail(DH_EINVAL, "the Laughlin wavefunction has no parameters");
   if (!h || !params) return fail(DH_EINVAL, "null argument");
   if (count != h->offsets.back()) return fail(DH_EINVAL, "parameter count mismatch");
   if (int rc = ensure_param_buffers(h)) return rc;
@@ -470,6 +547,7 @@ int dh_ref_layout(const dh_handle* h, size_t* offsets, int n) {
 }
 
 int dh_set_params_ref(dh_handle* h, const float* ref, size_t count, void* stream) {
+  if (h && h->laughlin) return count == 0 ? DH_OK : fail(DH_EINVAL, "the Laughlin wavefunction has no parameters");
   if (!h || !ref) return fail(DH_EINVAL, "null argument");
   if (count != h->ref_offsets.back()) return fail(DH_EINVAL, "reference parameter count mismatch");
   if (int rc = ensure_param_buffers(h)) return rc;
@@ -583,6 +661,29 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   return check_launch();
 }
 
+int ensure_expo(dh_handle* h) {
+  if (h->expo) return DH_OK;
+  HIP_TRY(hipMalloc(&h->expo, h->expo_host.size() * sizeof(int)));
+  HIP_TRY(hipMemcpy(h->expo, h->expo_host.data(), h->expo_host.size() * sizeof(int), hipMemcpyHostToDevice));
+  return DH_OK;
+}
+
+// log psi of nw walkers into logpsi [nw][2]: the Psiformer pass or the Laughlin kernel
+int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logpsi, hipStream_t s) {
+  if (h->laughlin) {
+    if (int rc = ensure_expo(h)) return rc;
+    PROF(PK_DET_VALUE, 0.0, 8.0 * nw * h->d.N);
+    launch_laughlin(h->d, x, h->expo, logpsi, nullptr, nullptr, nw, s);
+    return check_launch();
+  }
+  if (int rc = run_trunk(h, x, nw, 1, w, s)) return rc;
+  {
+    PROF(PK_DET_VALUE, 0.0, 4.0 * nw * h->d.N * h->d.ld_orb);
+    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s);
+  }
+  return check_launch();
+}
+
 int check_common(dh_handle* h, const void* x, int B, void* ws, size_t ws_bytes, size_t need) {
   if (!h) return fail(DH_EINVAL, "null handle");
   if (!h->params_set) return fail(DH_ESTATE, "parameters not set");
@@ -601,12 +702,7 @@ int dh_logpsi(dh_handle* h, const float* x, int B, float* logpsi, void* ws, size
   if (!logpsi) return fail(DH_EINVAL, "null output");
   hipStream_t s = (hipStream_t)stream;
   Work w = carve(h->d, B, 1, ws);
-  if (int rc = run_trunk(h, x, B, 1, w, s)) return rc;
-  {
-    PROF(PK_DET_VALUE, 0.0, 4.0 * B * h->d.N * h->d.ld_orb);
-    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, B, s);
-  }
-  return check_launch();
+  return value_pass(h, x, B, w, logpsi, s);
 }
 
 int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, int steps, float width, uint64_t seed,
@@ -619,11 +715,7 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
   const Dims& d = h->d;
   Work w = carve(d, B, 1, ws);
   // initial log-probability (mcmc.py:142)
-  if (int rc = run_trunk(h, x, B, 1, w, s)) return rc;
-  {
-    PROF(PK_DET_VALUE, 0.0, 4.0 * B * d.N * d.ld_orb);
-    launch_det_value(d, w.F, x, h->p.jastrow, h->norm, w.logpsi, B, s);
-  }
+  if (int rc = value_pass(h, x, B, w, w.logpsi, s)) return rc;
   launch_lp_from_logpsi(w.logpsi, lp, n_accept, B, s);
   const size_t nstride = (size_t)B * (2 * d.N + 1);
   for (int st = 0; st < steps; ++st) {
@@ -633,11 +725,7 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
       PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
       launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s);
     }
-    if (int rc = run_trunk(h, w.x2, B, 1, w, s)) return rc;
-    {
-      PROF(PK_DET_VALUE, 0.0, 4.0 * B * d.N * d.ld_orb);
-      launch_det_value(d, w.F, w.x2, h->p.jastrow, h->norm, w.logpsi, B, s);
-    }
+    if (int rc = value_pass(h, w.x2, B, w, w.logpsi, s)) return rc;
     {
       PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
       launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, step, walker_offset, nz, 0, s);
@@ -652,6 +740,13 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
   if (int rc = check_common(h, x, B, ws, ws_bytes, need1)) return rc;
   if (!e_l || !obs) return fail(DH_EINVAL, "null output");
   const Dims& d = h->d;
+  if (h->laughlin) {
+    if (int rc = ensure_expo(h)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    PROF(PK_DET_ENERGY, 0.0, 48.0 * B);
+    launch_laughlin(d, x, h->expo, nullptr, e_l, obs, B, s);
+    return check_launch();
+  }
   // largest chunk that fits the workspace
   int chunk = B;
   while (chunk > 1 && dh_workspace_bytes(h, chunk, 1) > ws_bytes) chunk = (chunk + 1) / 2;
@@ -872,6 +967,7 @@ int dh_logpsi_vjp(dh_handle* h, const float* x, int B, const float* ct, float* g
                   size_t ws_bytes, void* stream) {
   const size_t need1 = h ? dh_vjp_workspace_bytes(h, 1) : 0;
   if (int rc = check_common(h, x, B, ws, ws_bytes, need1)) return rc;
+  if (h && h->laughlin) return fail(DH_EINVAL, "the Laughlin wavefunction has no parameters to differentiate");
   if (!h->ref_set) return fail(DH_ESTATE, "the VJP needs parameters uploaded with dh_set_params_ref");
   if (!ct || !grad) return fail(DH_EINVAL, "null argument");
   if (h->d.D > 1024 || h->d.dh > 1024) return fail(DH_EINVAL, "VJP supports D <= 1024");

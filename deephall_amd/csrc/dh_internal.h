@@ -199,6 +199,12 @@ struct SparseBlocks {
 void launch_sparse_lll_grad(SparseBlocks blk, const float* dWfull, int ldw, const float* dbfull, int D, int NK, int M,
                             float* dWl, float* dbl, int acc, hipStream_t s);
 
+// laughlin.hip: log psi (e_l == nullptr) or the local energy (e_l [nw][2], obs [nw][8])
+// of the Laughlin wavefunction; expo [2][N] = (Q1 + m_j, Q1 - m_j)
+size_t laughlin_smem_bytes(int N);
+void launch_laughlin(const Dims& d, const float* x, const int* expo, float* logpsi, float* e_l, float* obs, int nw,
+                     hipStream_t s);
+
 // det.hip: backward of log psi = J + log sum_k det Phi_k for per-walker cotangents ct[nw][2]:
 // dF [nw*N][ld_orb] (all columns written) and jg[nw][2] = ct.re * dJ / d(ee_par, ee_anti)
 void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,

@@ -74,16 +74,7 @@ def make_local_kinetic_energy(f, Q: float, r):
     if spec.radius is None and abs(r - math.sqrt(Q)) < 1e-7 * max(1.0, r):
         knet = net
     else:
-        knet = Psiformer(
-            spec.nspins,
-            Q,
-            spec.ndets,
-            spec.num_heads,
-            spec.heads_dim,
-            spec.num_layers,
-            spec.orbital_type,
-            system=System(flux=spec.flux, radius=r, nspins=spec.nspins, interaction_strength=0.0),
-        )
+        knet = net.with_system(radius=r, interaction_strength=0.0)
 
     def ke(params, data):
         e_l, obs = _run_local_energy(knet, params, data)

@@ -3,14 +3,15 @@
 from __future__ import annotations
 
 from ..config import Network, NetworkType, System
+from .laughlin import Laughlin
 from .psiformer import Psiformer
 
 
 def make_network(system: System, network: Network) -> Psiformer:
     Q = system.flux / 2
     ntype = str(getattr(network.type, "value", network.type))
-    if ntype == NetworkType.laughlin.value:
-        raise NotImplementedError("the Laughlin network (networks/laughlin.py) is outside the MI355X hot path")
+    if ntype == NetworkType.laughlin.value:  # networks/__init__.py:24-27
+        return Laughlin(flux=system.flux, nspins=system.nspins, excitation_lz=system.lz_center, system=system)
     if ntype == NetworkType.psiformer.value:
         return Psiformer(
             Q=Q,
@@ -25,4 +26,4 @@ def make_network(system: System, network: Network) -> Psiformer:
     raise ValueError(f"unknown network type {network.type}")
 
 
-__all__ = ["make_network", "Psiformer"]
+__all__ = ["make_network", "Psiformer", "Laughlin"]

@@ -54,6 +54,9 @@ class NetworkSpec:
     radius: float | None = None
     interaction_strength: float = 1.0
     interaction_type: str = "coulomb"
+    network_type: str = "psiformer"
+    excitation_lz: float = 0.0
+    cf_flux: int = 1
 
     @property
     def nelec(self) -> int:
@@ -77,6 +80,9 @@ class NetworkSpec:
         c.num_heads, c.heads_dim, c.num_layers = self.num_heads, self.heads_dim, self.num_layers
         c.ndets = self.ndets
         c.orbital_type = {"full": 0, "sparse": 1}.get(str(getattr(self.orbital_type, "value", self.orbital_type)), -1)
+        c.network_type = {"psiformer": 0, "laughlin": 1}.get(str(getattr(self.network_type, "value", self.network_type)), -1)
+        c.excitation_lz = float(self.excitation_lz)
+        c.cf_flux = int(self.cf_flux)
         return c
 
 
@@ -180,6 +186,8 @@ def flatten_params(params) -> dict:
 
 def param_shapes(spec: NetworkSpec) -> dict:
     """Shapes of the reference's parameter tree (Flax auto-naming)."""
+    if spec.network_type == "laughlin":
+        return {}  # laughlin.py has no parameters
     D, H, dh = spec.D, spec.num_heads, spec.heads_dim
     M, N, K = spec.M, spec.nelec, spec.ndets
     p = "PsiformerLayers_0/"
@@ -394,6 +402,22 @@ class Psiformer:
             flat = self._flat_cache[key]
         h.set_params_ref(flat, key)
         return h
+
+    def with_system(self, radius=None, interaction_strength=None):
+        """The same network with another sphere radius / interaction strength (what
+        make_local_kinetic_energy(f, Q, r) evaluates, hamiltonian.py:83)."""
+        import dataclasses as _dc
+
+        other = object.__new__(type(self))
+        other.__dict__.update(self.__dict__)
+        kw = {}
+        if radius is not None:
+            kw["radius"] = float(radius)
+        if interaction_strength is not None:
+            kw["interaction_strength"] = float(interaction_strength)
+        other.spec = _dc.replace(self.spec, **kw)
+        other._flat_cache = {}
+        return other
 
     def invalidate(self):
         """Force the next call to re-upload the parameters (after updates that bypass the

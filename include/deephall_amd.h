@@ -52,6 +52,8 @@ extern "C" {
 
 #define DH_INTERACTION_COULOMB 0
 #define DH_INTERACTION_HARMONIC 1
+#define DH_NETWORK_PSIFORMER 0
+#define DH_NETWORK_LAUGHLIN 1 /* networks/laughlin.py: ground state and quasihole (no parameters) */
 #define DH_ORBITAL_FULL 0
 #define DH_ORBITAL_SPARSE 1 /* blocks.py:52-62: 8 features per (j, k) mixed into the M harmonics by
                                lll_weight; folded into the full layout when parameters are set */
@@ -68,6 +70,9 @@ typedef struct dh_config {
   int num_layers;             /* PsiformerNetwork.num_layers            */
   int ndets;                  /* PsiformerNetwork.determinants          */
   int orbital_type;           /* Network.orbital, DH_ORBITAL_*          */
+  int network_type;           /* Network.type, DH_NETWORK_*             */
+  float excitation_lz;        /* Laughlin: System.lz_center (networks/__init__.py:26) */
+  int cf_flux;                /* Laughlin: composite-fermion flux p (laughlin.py:23), >= 1 */
 } dh_config;
 
 typedef struct dh_handle dh_handle;

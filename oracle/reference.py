@@ -255,6 +255,109 @@ def logpsi(params, cfg: OracleConfig, x):
 
 
 # --------------------------------------------------------------------------
+# Laughlin wavefunction (networks/laughlin.py:19-100)
+# --------------------------------------------------------------------------
+
+
+@dataclass
+class LaughlinConfig:
+    """Laughlin(nspins, flux, cf_flux=1, excitation_lz) as networks/__init__.py:25-27 builds
+    it; plus the System fields local_energy reads."""
+
+    nspins: tuple = (3, 0)
+    flux: int = 6
+    excitation_lz: float = 0.0
+    cf_flux: int = 1
+    radius: float | None = None
+    interaction_strength: float = 1.0
+    interaction_type: str = "coulomb"
+
+    @property
+    def nelec(self):
+        return int(sum(self.nspins))
+
+    @property
+    def Q(self):
+        return self.flux / 2
+
+    @property
+    def r(self):
+        return self.radius if self.radius else math.sqrt(self.Q)
+
+    @property
+    def Q1(self):
+        return self.flux / 2 - self.cf_flux * (self.nelec - 1)
+
+    def kind(self):
+        """laughlin.py:32-45: ground state (N = 2 Q1 + 1), quasihole (N = 2 Q1),
+        quasiparticle (N = 2 Q1 + 2)."""
+        n, q1 = self.nelec, self.Q1
+        if n == 2 * q1 + 1:
+            return "ground"
+        if n == 2 * q1:
+            return "quasihole"
+        if n == 2 * q1 + 2:
+            return "quasiparticle"
+        raise ValueError("Filling not supported")
+
+    def exponents(self):
+        """m of the composite-fermion orbitals u^(Q1+m) v^(Q1-m) (laughlin.py:66-80)."""
+        q1, lz = self.Q1, self.excitation_lz
+        if self.kind() == "quasihole":
+            return np.concatenate([np.arange(-q1, -lz), np.arange(q1, -lz, -1)])
+        return np.arange(-q1, q1 + 1)
+
+
+def laughlin_orbitals(cfg: LaughlinConfig, x):
+    """laughlin.py:54-100 (complex [N, N])."""
+    theta, phi = x[..., 0], x[..., 1]
+    ctype = torch.complex128 if x.dtype == torch.float64 else torch.complex64
+    u = (torch.cos(theta / 2) * torch.exp(0.5j * phi.to(ctype)))[..., None]
+    v = (torch.sin(theta / 2) * torch.exp(-0.5j * phi.to(ctype)))[..., None]
+    N = cfg.nelec
+    q1 = cfg.Q1
+    element = u * v[:, 0] - u[:, 0] * v + torch.eye(N, dtype=ctype)
+    jastrow = torch.prod(element, dim=-1, keepdim=True)
+    if cfg.kind() != "quasiparticle":
+        m = cfg.exponents()
+        a = [int(round(q1 + mm)) for mm in m]
+        b = [int(round(q1 - mm)) for mm in m]
+        cols = torch.stack([u[:, 0] ** aa * v[:, 0] ** bb for aa, bb in zip(a, b)], -1)
+        return cols * jastrow
+    m = np.arange(-q1, q1 + 1)
+    cols = torch.stack([u[:, 0] ** int(round(q1 + mm)) * v[:, 0] ** int(round(q1 - mm)) for mm in m], -1)
+    jastrow_dv = jastrow * (torch.sum(-u[:, 0] / element, dim=-1, keepdim=True) + u)
+    jastrow_du = jastrow * (torch.sum(v[:, 0] / element, dim=-1, keepdim=True) - v)
+    m1 = cfg.excitation_lz
+    excited = (u ** int(round(q1 + m1)) * v ** int(round(q1 - m1))) * (
+        (q1 + 1 + m1) * v * jastrow_dv - (q1 + 1 - m1) * u * jastrow_du
+    )
+    return torch.cat([cols * jastrow, excited], -1)
+
+
+def laughlin_logpsi(cfg: LaughlinConfig, x):
+    """Laughlin.__call__ (laughlin.py:48-52): slogdet + log-sum-exp of one determinant."""
+    sign, logdet = torch.linalg.slogdet(laughlin_orbitals(cfg, x))
+    return torch.log(sign) + logdet
+
+
+def laughlin_local_energy(cfg: LaughlinConfig, xs):
+    """hamiltonian.local_energy with f = the Laughlin wavefunction (full autograd Hessian)."""
+    f = lambda p, y: laughlin_logpsi(cfg, y)  # noqa: E731
+    ke = make_local_kinetic_energy(f, cfg.Q, cfg.r)
+    els, obs = [], {}
+    for b in range(xs.shape[0]):
+        kin, o = ke(None, xs[b])
+        o = dict(o)
+        pot = potential(cfg, xs[b]) * cfg.interaction_strength
+        o["potential"], o["kinetic"] = pot, kin
+        els.append(kin + pot)
+        for k, v in o.items():
+            obs.setdefault(k, []).append(v)
+    return torch.stack(els), {k: torch.stack(v) for k, v in obs.items()}
+
+
+# --------------------------------------------------------------------------
 # Local energy (hamiltonian.py) — full Hessian, exactly the reference formulas
 # --------------------------------------------------------------------------
 
