@@ -15,6 +15,8 @@
 //   y    = scale * n  (+ bias on the value channel)
 // tanh_ch: y0 = tanh z0, y_t = tanh' z_t, y_L = tanh' z_L + tanh'' sum_t z_t^2,
 //          y_Sk = tanh' z_Sk + tanh'' (sum_t alpha_kt z_t)^2.
+#include <type_traits>
+
 #include "dh_internal.h"
 #include "device_common.h"
 
@@ -241,9 +243,11 @@ __global__ __launch_bounds__(256) void layernorm_value_kernel(const float* X, co
   }
 }
 
-// Channel rows, N <= 8, D = 256: ONE WAVE per (walker, electron).  Lane l owns columns
+// Channel rows, D = 256: ONE WAVE per (walker, electron).  Lane l owns columns
 // 4l..4l+3 of all C = 2N+5 channel rows in registers; every mean over D is a wave
-// reduction — no LDS, no barriers.  Same algebra as layernorm_kernel.
+// reduction — no LDS, no barriers.  Same algebra as layernorm_kernel.  The tanh branch
+// (mode 1) streams Z one channel at a time, so only the C pre-LN rows are held
+// (4C VGPRs: 180 at N = 20, one wave per SIMD there).
 template <int N>
 __global__ __launch_bounds__(256) void layernorm_ch_wave_kernel(const float* X, const float* __restrict__ Z,
                                                                 const float* __restrict__ ln,
@@ -272,34 +276,46 @@ __global__ __launch_bounds__(256) void layernorm_ch_wave_kernel(const float* X, 
 #pragma unroll
     for (int c = 0; c < C; ++c) z[c] = reinterpret_cast<const float4*>(X)[r4 + c * (D / 4)];
   } else {
-    float4 zz[C];
+    // y = h + tanh_ch(Z), componentwise; Z streamed channel by channel
+    const float4 z0 = reinterpret_cast<const float4*>(Z)[r4];
+    float4 y0, d1, d2;
+#define DH_TANH_D(F)          \
+  y0.F = tanhf(z0.F);         \
+  d1.F = 1.f - y0.F * y0.F;   \
+  d2.F = -2.f * y0.F * d1.F;
+    DH_TANH_D(x) DH_TANH_D(y) DH_TANH_D(z) DH_TANH_D(w)
+#undef DH_TANH_D
+    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f), uz[3];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      zz[c] = reinterpret_cast<const float4*>(Z)[r4 + c * (D / 4)];
-      z[c] = reinterpret_cast<const float4*>(h)[r4 + c * (D / 4)];
+    for (int k = 0; k < 3; ++k) uz[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    z[0] = reinterpret_cast<const float4*>(h)[r4];
+    z[0].x += y0.x;
+    z[0].y += y0.y;
+    z[0].z += y0.z;
+    z[0].w += y0.w;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float4 zt = reinterpret_cast<const float4*>(Z)[r4 + (1 + t) * (D / 4)];
+      z[1 + t] = reinterpret_cast<const float4*>(h)[r4 + (1 + t) * (D / 4)];
+#define DH_TANH_T(F)                        \
+  sq.F = fmaf(zt.F, zt.F, sq.F);            \
+  uz[0].F = fmaf(al[0][t], zt.F, uz[0].F);  \
+  uz[1].F = fmaf(al[1][t], zt.F, uz[1].F);  \
+  uz[2].F = fmaf(al[2][t], zt.F, uz[2].F);  \
+  z[1 + t].F = fmaf(d1.F, zt.F, z[1 + t].F);
+      DH_TANH_T(x) DH_TANH_T(y) DH_TANH_T(z) DH_TANH_T(w)
+#undef DH_TANH_T
     }
-    // y = h + tanh_ch(Z), componentwise
-#define DH_TANH_COMP(F)                                                         \
-  {                                                                             \
-    const float y0 = tanhf(zz[0].F);                                            \
-    const float d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;                        \
-    float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;                               \
-    _Pragma("unroll") for (int t = 0; t < T; ++t) {                             \
-      const float zt = zz[1 + t].F;                                             \
-      sq = fmaf(zt, zt, sq);                                                    \
-      u0 = fmaf(al[0][t], zt, u0);                                              \
-      u1 = fmaf(al[1][t], zt, u1);                                              \
-      u2 = fmaf(al[2][t], zt, u2);                                              \
-      z[1 + t].F += d1 * zt;                                                    \
-    }                                                                           \
-    z[0].F += y0;                                                               \
-    z[1 + T].F += d1 * zz[1 + T].F + d2 * sq;                                   \
-    z[2 + T].F += d1 * zz[2 + T].F + d2 * u0 * u0;                              \
-    z[3 + T].F += d1 * zz[3 + T].F + d2 * u1 * u1;                              \
-    z[4 + T].F += d1 * zz[4 + T].F + d2 * u2 * u2;                              \
-  }
-    DH_TANH_COMP(x) DH_TANH_COMP(y) DH_TANH_COMP(z) DH_TANH_COMP(w)
-#undef DH_TANH_COMP
+#pragma unroll
+    for (int c = 1 + T; c < C; ++c) {
+      const float4 zc = reinterpret_cast<const float4*>(Z)[r4 + c * (D / 4)];
+      z[c] = reinterpret_cast<const float4*>(h)[r4 + c * (D / 4)];
+      const float4 w = (c == 1 + T) ? sq : uz[c - 2 - T];
+      const bool L = c == 1 + T;
+#define DH_TANH_O(F) z[c].F += d1.F * zc.F + d2.F * (L ? w.F : w.F * w.F);
+      DH_TANH_O(x) DH_TANH_O(y) DH_TANH_O(z) DH_TANH_O(w)
+#undef DH_TANH_O
+    }
   }
   // channel means, centre
 #pragma unroll
@@ -371,6 +387,159 @@ __global__ __launch_bounds__(256) void layernorm_ch_wave_kernel(const float* X, 
   for (int k = 0; k < 3; ++k) out[(2 + T + k) * (D / 4)] = oS[k];
 }
 
+// Channel rows for large N (C = 2N+5 up to 45), D = 256: FOUR WAVES per (walker,
+// electron), wave w owning columns 64w..64w+63 (one float per lane per channel row, C
+// VGPRs instead of 4C), so several electrons share a SIMD.  The C + (C + T + 3) sums over
+// D are transposed through a per-wave LDS scratch 16 rows at a time (16 writes, 16 reads
+// and 2 shuffles per 16 sums instead of 6 shuffles per sum), then the four waves'
+// partials are combined through LDS (two barriers in all).
+template <int N>
+__global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, const float* __restrict__ Z,
+                                                                const float* __restrict__ ln,
+                                                                const float* __restrict__ geo, float* h, int ne,
+                                                                int mode) {
+  constexpr int T = 2 * N, C = 2 * N + 5, D = 256, NR = C + T + 3;
+  __shared__ float red[4][C + NR];
+  __shared__ float al[3][T];       // flow coefficients (broadcast reads)
+  __shared__ float tb[4][16 * 65];  // per-wave transpose scratch
+  const int e = blockIdx.x;         // walker*N + electron
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = e / N;
+  if (threadIdx.x < N) {
+    const int i = threadIdx.x;
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    al[0][2 * i] = -g.z;
+    al[1][2 * i] = g.w;
+    al[2][2 * i] = 0.f;
+    al[0][2 * i + 1] = -(g.y * g.w);
+    al[1][2 * i + 1] = -(g.y * g.z);
+    al[2][2 * i + 1] = g.x;
+  }
+  __syncthreads();
+  float* tw = tb[w];
+  // sums over this wave's 64 columns of R per-lane values getv(r) -> dst[r]
+  auto rows_sum = [&](auto getv, auto R_, float* dst) {
+    constexpr int R = decltype(R_)::value;
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0 += 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (r0 + j < R) tw[j * 65 + lane] = getv(r0 + j);
+      __builtin_amdgcn_wave_barrier();
+      const int j = lane >> 2, q = lane & 3;
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v += tw[j * 65 + 16 * q + m];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      if (q == 0 && r0 + j < R) dst[r0 + j] = v;
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
+  const size_t r0 = (size_t)e * C * D + 64 * w + lane;  // (row e*C, this lane's column)
+  float z[C];
+  if (mode == 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) z[c] = X[r0 + (size_t)c * D];
+  } else {
+    const float zz0 = Z[r0];
+    const float y0 = tanhf(zz0), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
+    float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+    z[0] = h[r0] + y0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float zt = Z[r0 + (size_t)(1 + t) * D];
+      sq = fmaf(zt, zt, sq);
+      u0 = fmaf(al[0][t], zt, u0);
+      u1 = fmaf(al[1][t], zt, u1);
+      u2 = fmaf(al[2][t], zt, u2);
+      z[1 + t] = fmaf(d1, zt, h[r0 + (size_t)(1 + t) * D]);
+    }
+    z[1 + T] = h[r0 + (size_t)(1 + T) * D] + d1 * Z[r0 + (size_t)(1 + T) * D] + d2 * sq;
+    const float uu[3] = {u0, u1, u2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const size_t rc = r0 + (size_t)(2 + T + k) * D;
+      z[2 + T + k] = h[rc] + d1 * Z[rc] + d2 * uu[k] * uu[k];
+    }
+  }
+  // channel means
+  __shared__ float mu[C];
+  rows_sum([&](int c) { return z[c]; }, std::integral_constant<int, C>{}, red[w]);
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    mu[c] = ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) * (1.f / D);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < C; ++c) z[c] -= mu[c];
+  float u[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    u[k] = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) u[k] = fmaf(al[k][t], z[1 + t], u[k]);
+  }
+  // p_c = mean(z0 z_c), q_t = mean(z_t^2), uu_k = mean(u_k^2)
+  rows_sum(
+      [&](int r) {
+        if (r < C) return z[0] * z[r];
+        if (r < C + T) return z[1 + r - C] * z[1 + r - C];
+        return u[r - C - T] * u[r - C - T];
+      },
+      std::integral_constant<int, NR>{}, red[w] + C);
+  __syncthreads();
+  // coefficients, once per electron (wave 0): fin = the D-means, at_t, cl, au_k, cs_k
+  __shared__ float fin[NR], cf[T + 12];
+  for (int r = threadIdx.x; r < NR; r += 256)
+    fin[r] = ((red[0][C + r] + red[1][C + r]) + (red[2][C + r] + red[3][C + r])) * (1.f / D);
+  __syncthreads();
+  const float s = 1.f / sqrtf(fin[0] + 1e-5f), s2 = s * s;
+  if (w == 0) {
+    float clv = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    if (lane < T) {
+      const float at = s2 * fin[1 + lane];
+      cf[lane] = at;
+      clv = 3.f * at * at - s2 * fin[C + lane];
+      a0 = al[0][lane] * at;
+      a1 = al[1][lane] * at;
+      a2 = al[2][lane] * at;
+    }
+    clv = wave_sum(clv);
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    a2 = wave_sum(a2);
+    if (lane == 0) {
+      cf[T] = clv;
+      cf[T + 1] = s2 * fin[1 + T];  // aL
+      const float au[3] = {a0, a1, a2};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        cf[T + 2 + k] = au[k];
+        cf[T + 5 + k] = 3.f * au[k] * au[k] - s2 * fin[C + T + k];
+        cf[T + 8 + k] = s2 * fin[2 + T + k];  // aS_k
+      }
+    }
+  }
+  __syncthreads();
+  const int col = 64 * w + lane;
+  const float g = ln[col], bb = ln[D + col], gs = g * s, z0 = z[0];
+  float sat = 0.f;
+  h[r0] = g * (s * z0) + bb;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const float at = cf[t];
+    sat = fmaf(at, z[1 + t], sat);
+    h[r0 + (size_t)(1 + t) * D] = gs * (z[1 + t] - at * z0);
+  }
+  h[r0 + (size_t)(1 + T) * D] = gs * (z[1 + T] - cf[T + 1] * z0 - 2.f * sat + cf[T] * z0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    h[r0 + (size_t)(2 + T + k) * D] =
+        gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
+}
+
 template <int N>
 void launch_ln_wave(const float* X, const float* Z, const float* ln, const float* geo, float* h, int ne, int mode,
                     hipStream_t s) {
@@ -381,9 +550,15 @@ void launch_ln_wave(const float* X, const float* Z, const float* ln, const float
 
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
                       int nw, int C, int mode, hipStream_t s) {
-  if (C > 1 && d.D == 256 && d.N <= 8) {
+  if (C > 1 && d.D == 256 && (d.N <= 8 || d.N == 10 || d.N == 20)) {
     const int ne = nw * d.N;
     switch (d.N) {
+      case 10:
+        hipLaunchKernelGGL(layernorm_ch_quad_kernel<10>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode);
+        return;
+      case 20:
+        hipLaunchKernelGGL(layernorm_ch_quad_kernel<20>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode);
+        return;
       case 1: launch_ln_wave<1>(X, Z, ln, geo, h, ne, mode, s); return;
       case 2: launch_ln_wave<2>(X, Z, ln, geo, h, ne, mode, s); return;
       case 3: launch_ln_wave<3>(X, Z, ln, geo, h, ne, mode, s); return;
