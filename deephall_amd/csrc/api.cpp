@@ -608,7 +608,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // Layer-1 q|k|v come straight from the K=4 features through the folded W0 Wqkv: inside
   // the attention kernel when it supports that (fused), else written by the input kernel.
   const bool fold = d.L > 0;
-  const bool fused = fold && attention_takes_features(d);
+  const bool fused = fold && attention_takes_features(d, C);
   // log psi, split-bf16: layer 1's residual h = features W0 is formed in the epilogue of
   // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
   const bool h_feat = C == 1 && fused && x6 && ln_fused;

@@ -1066,13 +1066,20 @@ void launch_ch(const Dims& d, const float* qkv, const float* geo, float* o, int 
 // wave kernels: every N <= 8, plus the N = 10 and N = 20 instances of BASELINE.json's
 // C4 / C5 configs (one wave per (walker, head) there too: 2x / 10x faster than the
 // 256-thread channel kernel v2, whose three barriers per channel dominate)
-bool attention_takes_features(const Dims& d) { return d.dh == 64 && (d.N <= 8 || d.N == 10 || d.N == 20); }
+bool attention_takes_features(const Dims& d, int C) {
+  if (C > 1 && attention_mfma_supported(d)) return false;  // the MFMA kernel reads q|k|v rows
+  return d.dh == 64 && (d.N <= 8 || d.N == 10 || d.N == 20);
+}
 
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
                       const float* W0qkv, const float* bqkv) {
   // wave kernels (value and channel) for dh = 64, N <= 8; W0qkv != nullptr selects the
   // fused layer-1 form (q|k|v from the input features), valid only for those kernels.
-  if (attention_takes_features(d)) {
+  if (C > 1 && attention_mfma_supported(d)) {
+    launch_attention_mfma(d, qkv, geo, o, nw, s);
+    return;
+  }
+  if (attention_takes_features(d, C)) {
     switch (d.N) {
       case 1: launch_wave<1>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
       case 2: launch_wave<2>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;

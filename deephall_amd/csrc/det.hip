@@ -229,6 +229,7 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       const size_t row = (size_t)b * N + i;
       cf acc{0.f, 0.f};
+      #pragma unroll 8
       for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
       A[idx] = acc;
     }
@@ -374,6 +375,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
   float* Fc = sm + L.Fc;
   cf* LB2 = (cf*)(sm + L.LB2);
   constexpr bool STAGED = PF > 0;
+  constexpr int kUnrollM = STAGED ? 1 : 8;  // unstaged: 8 independent F loads in flight per thread
   constexpr int PFMAX = STAGED ? PF : 1;
   float pf[PFMAX];
   auto stage_load = [&](int c) {
@@ -457,6 +459,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
       const int i = idx / N, j = idx % N;
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       cf acc{0.f, 0.f};
+      #pragma unroll kUnrollM
       for (int p = 0; p < M; ++p)
         cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
       Aug[i * 2 * N + j] = acc;
@@ -492,6 +495,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const float thh[3] = {ct * cp, ct * sp, -st};
         cf acc{0.f, 0.f}, g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
         cf lb2{0.f, 0.f};
+        #pragma unroll kUnrollM
         for (int p = 0; p < M; ++p) {
           const cf f = STAGED ? fs(Fc, i, p, j, kd) : F.at(rt, blk, p, j, kd);
           const cf dth = DTH[i * M + p], dph = DPH[i * M + p];
@@ -554,12 +558,14 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const size_t r0 = rowbase + (size_t)i * C;
         cf acc{0.f, 0.f}, acc2{0.f, 0.f};
         if constexpr (STAGED) {
+          #pragma unroll kUnrollM
           for (int p = 0; p < M; ++p) {
             cfma(acc, fs(Fc, i, p, j, kd), E0[i * M + p]);
             cfma(acc, fs(Fv, i, p, j, kd), LBe[i * M + p]);
           }
           acc2 = LB2[idx];
         } else {
+          #pragma unroll kUnrollM
           for (int p = 0; p < M; ++p) {
             cfma(acc, F.at(r0 + 1 + T, blk, p, j, kd), E0[i * M + p]);
             cfma(acc, F.at(r0, blk, p, j, kd), LBe[i * M + p]);
@@ -590,6 +596,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const size_t r0 = rowbase + (size_t)i * C;
         const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
         cf acc{0.f, 0.f};
+        #pragma unroll kUnrollM
         for (int p = 0; p < M; ++p) {
           const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
           const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
@@ -890,6 +897,7 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       const size_t row = (size_t)b * N + i;
       cf acc{0.f, 0.f};
+      #pragma unroll 8
       for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
       A[i * lda + j] = acc;
       if (lda > N) A[i * lda + N + j] = cf{i == j ? 1.f : 0.f, 0.f};

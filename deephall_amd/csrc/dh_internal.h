@@ -125,7 +125,10 @@ void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t
 // attention.hip: channel self-attention for all heads.
 // W0qkv/bqkv non-null: layer-1 q|k|v formed in-kernel from the input features (only when
 // attention_takes_features(d)); otherwise read from qkv [rows][3D].
-bool attention_takes_features(const Dims& d);
+bool attention_takes_features(const Dims& d, int C);
+// channel attention on the matrix cores (attention_mfma.hip): C > 1, dh = 64, N = 10, 20
+bool attention_mfma_supported(const Dims& d);
+void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s);
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
                       const float* W0qkv = nullptr, const float* bqkv = nullptr);
 
