@@ -758,7 +758,9 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
     if (int rc = run_trunk(h, xc, nw, d.C, w, s)) return rc;
     {
       PROF(PK_DET_ENERGY, 0.0, 4.0 * nw * d.N * d.C * d.ld_orb);
-      launch_det_energy(d, w.F, xc, w.geo, h->p.jastrow, h->norm, e_l + 2 * (size_t)b0, obs + 8 * (size_t)b0, nw, s);
+      // the trunk's o buffer (rows x D floats) is free here and holds nw K C N N complex when 2 K N <= D
+      launch_det_energy(d, w.F, xc, w.geo, h->p.jastrow, h->norm, e_l + 2 * (size_t)b0, obs + 8 * (size_t)b0, nw, s,
+                        det_precontract(d) ? w.o : nullptr);
     }
     if (int rc = check_launch()) return rc;
   }

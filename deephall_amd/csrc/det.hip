@@ -15,6 +15,8 @@
 // with Phi channels from the product rule of F and the envelope leaves, then
 // Jastrow, potential and the KE / Lz / Lz^2 / L^2 assembly (DESIGN.md §3.4,
 // equivalent to hamiltonian.py:115-169).
+#include <cstdlib>
+
 #include "dh_internal.h"
 #include "device_common.h"
 
@@ -180,7 +182,12 @@ __device__ inline double jastrow_pair(double r, double al, double cst, double* f
 }
 
 // ------------------------------------------------------------------ value kernel
-__global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+// The orbital matrix is contracted row by row: lane (j, g) sums harmonics m = g + G u
+// (G = 64 / N lane groups, u < MGV, all loads of a row in flight at once, one wave load
+// instruction covering G consecutive harmonics = 4 G N contiguous bytes), groups combined
+// with shuffles.
+template <int MGV>
+__global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                  const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
                                  int N, int n_up, int M, int K) {
   extern __shared__ float sm_raw[];
@@ -191,7 +198,6 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
   cf* logdet = ld + K;
   int* piv = reinterpret_cast<int*>(logdet + 1);
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const FView F{Fp, ldF, M, N, K};
   double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] unit vectors (double: close pairs)
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
@@ -223,15 +229,38 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
     }
     for (int o = 32; o > 0; o >>= 1) Jw += __shfl_xor(Jw, o, 64);
   }
+  const int G = 64 / N, gj = tid % N, gg = tid / N, NK = N * K, MNK = M * NK;
   for (int k = 0; k < K; ++k) {
-    for (int idx = tid; idx < N * N; idx += nt) {
-      const int i = idx / N, j = idx % N;
+    if constexpr (MGV == 0) {  // small rows: one thread per entry, serial over m
+      for (int idx = tid; idx < N * N; idx += nt) {
+        const int i = idx / N, j = idx % N;
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        const float* rp = Fp + ((size_t)b * N + i) * ldF + (size_t)blk * 2 * MNK + (size_t)j * K + k;
+        cf acc{0.f, 0.f};
+        for (int p = 0; p < M; ++p) cfma(acc, cf{rp[(size_t)p * NK], rp[(size_t)MNK + (size_t)p * NK]}, E0[i * M + p]);
+        A[idx] = acc;
+      }
+    }
+    for (int i = 0; i < (MGV == 0 ? 0 : N); ++i) {
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
-      const size_t row = (size_t)b * N + i;
+      const float* rp = Fp + ((size_t)b * N + i) * ldF + (size_t)blk * 2 * MNK + (size_t)gj * K + k;
+      float f[2 * (MGV > 0 ? MGV : 1)];
+#pragma unroll
+      for (int u = 0; u < MGV; ++u) {
+        const int m = gg + G * u;
+        const bool ok = gg < G && m < M;
+        f[2 * u] = ok ? rp[(size_t)m * NK] : 0.f;
+        f[2 * u + 1] = ok ? rp[(size_t)MNK + (size_t)m * NK] : 0.f;
+      }
       cf acc{0.f, 0.f};
-      #pragma unroll 8
-      for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
-      A[idx] = acc;
+#pragma unroll
+      for (int u = 0; u < MGV; ++u) cfma(acc, cf{f[2 * u], f[2 * u + 1]}, E0[i * M + min(gg + G * u, M - 1)]);
+      float re = acc.re, im = acc.im;
+      for (int q = 1; q < G; ++q) {
+        re += __shfl(acc.re, gj + N * q, 64);
+        im += __shfl(acc.im, gj + N * q, 64);
+      }
+      if (gg == 0) A[i * N + gj] = cf{re, im};
     }
     __syncthreads();
     eliminate(A, N, N, N, false, fac, piv, logdet);
@@ -253,6 +282,199 @@ __global__ void det_value_kernel(const float* __restrict__ Fp, int ldF, const fl
     logpsi[2 * b] = val_re + (float)Jw;
     logpsi[2 * b + 1] = val_im;
   }
+}
+
+// ------------------------------------------------------------------ envelope contraction
+// For large orbital rows (2 M N K floats per channel row, C5: 2320) det_energy_kernel no
+// longer contracts F itself: this kernel forms, per (walker, det kd, channel c), the
+// complex N x N matrices it needs (blocks.py:64-68 with the product rule):
+//   c = 0:       Phi0   = sum_m F_0 e0
+//   c = 1+t:     Phi_t  = sum_m F_t e0 + [t moves i] sum_m F_0 de/dt
+//   c = 1+T:     Phi_L  = sum_m F_L e0 + sum_m F_0 LB(e) + 2 sum_{t moves i} sum_m F_t de/dt
+//   c = 2+T+k:   Phi_Sk = sum_m F_Sk e0 + sum_m F_0 e_flow2,k
+//                         + 2 sum_t alpha_kt sum_m F_t (phh_k de/dth - thh_k de/dph)
+// into PhiC[((b K + kd) C + c) N N + i N + j] (re, im).  One 256-thread workgroup per
+// (walker, electron i).  Every term is linear in the harmonic sums, so each of the 4 G lane
+// groups (lane (j, g) of wave w, group gg = G w + g, G = 64 / N) forms ALL of them over its
+// own harmonics m = gg + 4 G u (u < MG) — partial extras included — and the partials are
+// summed at the end (shuffles within a wave, LDS across the four).  A wave load instruction
+// covers G consecutive harmonics = 4 G N contiguous bytes.  The channel rows stream through
+// a per-wave LDS-DMA ring (global_load_lds_dword, RING rows deep: RING - 1 rows in flight
+// without holding registers), counted with vmcnt; every lane reads back only its own words.
+// LDS-DMA ring depth: up to 4 rows, (depth - 1) rows of 2 MG loads within vmcnt's 6 bits
+__host__ __device__ constexpr int env_ring(int MG) { return (63 / (2 * MG) + 1) < 4 ? (63 / (2 * MG) + 1) : 4; }
+
+template <int MG>
+__global__ __launch_bounds__(256) void env_contract_kernel(const float* __restrict__ Fp, int ldF,
+                                                           const float* __restrict__ x,
+                                                           const float* __restrict__ geo_g,
+                                                           const float* __restrict__ norm, float* __restrict__ PhiC,
+                                                           int nw, int N, int n_up, int M, int K, float Q) {
+  constexpr int Q2 = 2 * MG, RING = env_ring(MG);  // load instructions per row, rows per ring
+  static_assert((RING - 1) * Q2 <= 63, "vmcnt range");
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x / N, i = blockIdx.x - (blockIdx.x / N) * N;
+  const int T = 2 * N, C = 2 * N + 5;
+  cf* wt = reinterpret_cast<cf*>(sm);         // [E0, DTH, DPH, LB, W0..2, SF0..2][M]
+  cf* part = wt + 10 * M;                     // [4 waves][C][N] partial sums
+  float* al = reinterpret_cast<float*>(part + 4 * C * N);  // [3][T]
+  float* ring = al + ((3 * T + 3) & ~3);      // [4 waves][RING][Q2][64]
+  {
+    const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const float gauge = ct >= 0.f ? Q : -Q;
+    const float th = x[2 * (b * N + i)], ph = x[2 * (b * N + i) + 1];
+    const float phh[3] = {-sp, cp, 0.f};
+    const float thh[3] = {ct * cp, ct * sp, -st};
+    for (int p = tid; p < M; p += 256) {
+      const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge);
+      wt[p] = e.e0;
+      wt[M + p] = e.dth;
+      wt[2 * M + p] = e.dph;
+      wt[3 * M + p] = e.lb;
+      const float mf = (float)p - 0.5f * (float)(M - 1) - gauge;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        wt[(4 + k) * M + p] = cf{phh[k] * e.dth.re - thh[k] * e.dph.re, phh[k] * e.dth.im - thh[k] * e.dph.im};
+        wt[(7 + k) * M + p] = env_flow2(e.e0, e.dth, e.d2th, mf, st, ct, sp, cp, k);
+      }
+    }
+    if (tid < T) {  // alpha_kt from the geometry of the electron tangent t moves
+      const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (tid >> 1)));
+      al[tid] = (tid & 1) ? -(ga.y * ga.w) : -ga.z;
+      al[T + tid] = (tid & 1) ? -(ga.y * ga.z) : ga.w;
+      al[2 * T + tid] = (tid & 1) ? ga.x : 0.f;
+    }
+  }
+  __syncthreads();
+  const int G = 64 / N, j = lane % N, g = lane / N, S = 4 * G;
+  const int gg = G * wv + g;
+  const bool act = g < G;
+  const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+  const int NK = N * K, MNK = M * NK;
+  auto gsum = [&](float v) __attribute__((always_inline)) {
+    float r = v;
+    for (int q = 1; q < G; ++q) r += __shfl(v, j + N * q, 64);
+    return r;
+  };
+  auto gsumc = [&](cf v) __attribute__((always_inline)) { return cf{gsum(v.re), gsum(v.im)}; };
+  const float* rowbase = Fp + ((size_t)(b * N + i) * C) * ldF + (size_t)blk * 2 * MNK + (size_t)j * K;
+  // lane's harmonic u (< MG) is m = gg + S u, valid when m < M (and g < G)
+  auto mw = [&](int u) __attribute__((always_inline)) { return min(gg + S * u, M - 1); };
+  auto okm = [&](int u) __attribute__((always_inline)) { return act && gg + S * u < M; };
+  float* wring = ring + (size_t)wv * RING * Q2 * 64;
+  const uint32_t ring0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)wring);
+  // DMA row c of det kd into ring slot c % RING
+  auto issue = [&](int c, int kd) __attribute__((always_inline)) {
+    const float* rp = rowbase + (size_t)c * ldF + kd;
+    const int slot = c % RING;
+#pragma unroll
+    for (int q = 0; q < Q2; ++q) {
+      const int u = q >> 1;
+      const float* src = okm(u) ? rp + ((q & 1) ? (size_t)MNK : 0) + (size_t)(gg + S * u) * NK : rowbase;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + (uint32_t)((slot * Q2 + q) * 256));
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  };
+  // wait until row c landed (rows issued after it: min(RING - 1, C - 1 - c))
+  auto wait_row = [&](int c) __attribute__((always_inline)) {
+    const int ahead = min(RING - 1, C - 1 - c);
+    if constexpr (RING >= 4) {
+      if (ahead >= 3) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * Q2) : "memory");
+        return;
+      }
+    }
+    if constexpr (RING >= 3) {
+      if (ahead == 2) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * Q2) : "memory");
+        return;
+      }
+    }
+    if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q2) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto fval = [&](int c, int u) __attribute__((always_inline)) {
+    const float* r = wring + (size_t)((c % RING) * Q2 + 2 * u) * 64 + lane;
+    return okm(u) ? cf{r[0], r[64]} : cf{0.f, 0.f};
+  };
+  for (int kd = 0; kd < K; ++kd) {
+    cf xd{0.f, 0.f}, xp{0.f, 0.f}, xl{0.f, 0.f}, xs0{0.f, 0.f}, xs1{0.f, 0.f}, xs2{0.f, 0.f};  // F_0 extras
+    cf lb2{0.f, 0.f}, gu0{0.f, 0.f}, gu1{0.f, 0.f}, gu2{0.f, 0.f};                            // lane partials
+    for (int c = 0; c < RING - 1 && c < C; ++c) issue(c, kd);
+    for (int c = 0; c < C; ++c) {
+      if (c + RING - 1 < C) issue(c + RING - 1, kd);  // its slot's last reader was row c - 1
+      wait_row(c);
+      const bool tang = c >= 1 && c <= T;
+      const int t = c - 1;
+      const bool own = tang && (t >> 1) == i;
+      cf e0a{0.f, 0.f};
+      if (c == 0) {
+#pragma unroll
+        for (int u = 0; u < MG; ++u) {
+          const cf fv = fval(c, u);
+          const int m = mw(u);
+          cfma(e0a, fv, wt[m]);
+          cfma(xd, fv, wt[M + m]);
+          cfma(xp, fv, wt[2 * M + m]);
+          cfma(xl, fv, wt[3 * M + m]);
+          cfma(xs0, fv, wt[7 * M + m]);
+          cfma(xs1, fv, wt[8 * M + m]);
+          cfma(xs2, fv, wt[9 * M + m]);
+        }
+      } else if (tang) {
+        cf w0{0.f, 0.f}, w1{0.f, 0.f}, w2{0.f, 0.f}, dd{0.f, 0.f};
+        const cf* wdd = wt + ((t & 1) ? 2 : 1) * M;
+#pragma unroll
+        for (int u = 0; u < MG; ++u) {
+          const cf fv = fval(c, u);
+          const int m = mw(u);
+          cfma(e0a, fv, wt[m]);
+          cfma(w0, fv, wt[4 * M + m]);
+          cfma(w1, fv, wt[5 * M + m]);
+          cfma(w2, fv, wt[6 * M + m]);
+          if (own) cfma(dd, fv, wdd[m]);
+        }
+        gu0 += al[t] * w0;
+        gu1 += al[T + t] * w1;
+        gu2 += al[2 * T + t] * w2;
+        lb2 += dd;
+        if (own) e0a += (t & 1) ? xp : xd;
+      } else {
+#pragma unroll
+        for (int u = 0; u < MG; ++u) cfma(e0a, fval(c, u), wt[mw(u)]);
+        if (c == T + 1) e0a += xl + 2.f * lb2;
+        if (c >= T + 2) {
+          const int k = c - T - 2;
+          e0a += (k == 0 ? xs0 : (k == 1 ? xs1 : xs2)) + 2.f * (k == 0 ? gu0 : (k == 1 ? gu1 : gu2));
+        }
+      }
+      const cf v = gsumc(e0a);
+      if (g == 0) part[((size_t)wv * C + c) * N + j] = v;
+    }
+    __syncthreads();
+    float* out = PhiC + 2 * ((size_t)(b * K + kd) * C * N * N + (size_t)i * N);
+    for (int e = tid; e < C * N; e += 256) {
+      const int c = e / N, jj = e - (e / N) * N;
+      const cf v = (part[e] + part[C * N + e]) + (part[2 * C * N + e] + part[3 * C * N + e]);
+      out[2 * ((size_t)c * N * N + jj)] = v.re;
+      out[2 * ((size_t)c * N * N + jj) + 1] = v.im;
+    }
+    __syncthreads();
+  }
+}
+
+// dynamic LDS of env_contract_kernel<MG>
+size_t env_contract_smem(int N, int M, int MG) {
+  const int T = 2 * N, C = 2 * N + 5;
+  return (size_t)(20 * M + 8 * C * N + ((3 * T + 3) & ~3) + 4 * env_ring(MG) * 2 * MG * 64) * sizeof(float);
 }
 
 // ------------------------------------------------------------------ energy kernel
@@ -344,12 +566,14 @@ __device__ inline void block_sum4(float v[4], float* red) {
   __syncthreads();
 }
 
-template <int PF>  // PF > 0: orbital rows staged through LDS, PF floats per thread in flight
+// PF > 0: orbital rows staged through LDS, PF floats per thread in flight.
+// PC: the channel matrices come precontracted from env_contract_kernel (PhiC), F unused.
+template <int PF, bool PC = false>
 __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                   const float* __restrict__ geo_g, const float* __restrict__ jas,
                                   const float* __restrict__ norm, float* __restrict__ e_l, float* __restrict__ obs,
                                   int N, int n_up, int M, int K, float Q, float radius, float lambda,
-                                  int interaction) {
+                                  int interaction, const float* __restrict__ PhiC) {
   extern __shared__ float sm[];
   const int T = 2 * N, C = 2 * N + 5, NN = N * N;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -366,6 +590,10 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
   int* piv = reinterpret_cast<int*>(sm + L.misc);
   cf* logdet = reinterpret_cast<cf*>(sm + L.misc + 2);
   const FView F{Fp, ldF, M, N, K};
+  auto phic = [&](int kd, int c, int idx) -> cf {
+    const float* q = PhiC + 2 * (((size_t)(b * K + kd) * C + c) * NN + idx);
+    return cf{q[0], q[1]};
+  };
   const size_t rowbase = (size_t)b * N * C;  // row of (b, i, c) = rowbase + i*C + c
   // ---- staging of orbital rows (STAGED): the N rows of one channel, each the electron's
   // own spin block (2 M N K floats), through registers into LDS.  The value rows stay in
@@ -375,7 +603,6 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
   float* Fc = sm + L.Fc;
   cf* LB2 = (cf*)(sm + L.LB2);
   constexpr bool STAGED = PF > 0;
-  constexpr int kUnrollM = STAGED ? 1 : 8;  // unstaged: 8 independent F loads in flight per thread
   constexpr int PFMAX = STAGED ? PF : 1;
   float pf[PFMAX];
   auto stage_load = [&](int c) {
@@ -437,7 +664,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
       al[k * T + t] = a;
     }
   }
-  for (int idx = tid; idx < N * M; idx += nt) {
+  for (int idx = tid; idx < (PC ? 0 : N * M); idx += nt) {
     const int i = idx / M, p = idx % M;
     const float gauge = (geo[4 * i + 1] >= 0.f ? Q : -Q);
     const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true, gauge);
@@ -459,9 +686,11 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
       const int i = idx / N, j = idx % N;
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       cf acc{0.f, 0.f};
-      #pragma unroll kUnrollM
-      for (int p = 0; p < M; ++p)
-        cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
+      if constexpr (PC)
+        acc = phic(kd, 0, idx);
+      else
+        for (int p = 0; p < M; ++p)
+          cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(rowbase + (size_t)i * C, blk, p, j, kd), E0[i * M + p]);
       Aug[i * 2 * N + j] = acc;
       Aug[i * 2 * N + N + j] = (i == j) ? cf{1.f, 0.f} : cf{0.f, 0.f};
     }
@@ -486,7 +715,8 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         stage_load(t + 1 < T ? t + 2 : T + 1);
         __syncthreads();
       }
-      for (int idx = tid; idx < NN; idx += nt) {
+      for (int idx = tid; idx < (PC ? NN : 0); idx += nt) Phi[idx] = phic(kd, 1 + t, idx);
+      for (int idx = tid; idx < (PC ? 0 : NN); idx += nt) {
         const int i = idx / N, j = idx % N;
         const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
         const size_t rt = rowbase + (size_t)i * C + 1 + t;
@@ -495,7 +725,6 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const float thh[3] = {ct * cp, ct * sp, -st};
         cf acc{0.f, 0.f}, g0{0.f, 0.f}, g1{0.f, 0.f}, g2{0.f, 0.f};
         cf lb2{0.f, 0.f};
-        #pragma unroll kUnrollM
         for (int p = 0; p < M; ++p) {
           const cf f = STAGED ? fs(Fc, i, p, j, kd) : F.at(rt, blk, p, j, kd);
           const cf dth = DTH[i * M + p], dph = DPH[i * M + p];
@@ -557,15 +786,15 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
         const size_t r0 = rowbase + (size_t)i * C;
         cf acc{0.f, 0.f}, acc2{0.f, 0.f};
-        if constexpr (STAGED) {
-          #pragma unroll kUnrollM
+        if constexpr (PC) {
+          acc = phic(kd, 1 + T, idx);  // includes 2 LB2
+        } else if constexpr (STAGED) {
           for (int p = 0; p < M; ++p) {
             cfma(acc, fs(Fc, i, p, j, kd), E0[i * M + p]);
             cfma(acc, fs(Fv, i, p, j, kd), LBe[i * M + p]);
           }
           acc2 = LB2[idx];
         } else {
-          #pragma unroll kUnrollM
           for (int p = 0; p < M; ++p) {
             cfma(acc, F.at(r0 + 1 + T, blk, p, j, kd), E0[i * M + p]);
             cfma(acc, F.at(r0, blk, p, j, kd), LBe[i * M + p]);
@@ -596,14 +825,17 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
         const size_t r0 = rowbase + (size_t)i * C;
         const float st = geo[4 * i], ct = geo[4 * i + 1], sp = geo[4 * i + 2], cp = geo[4 * i + 3];
         cf acc{0.f, 0.f};
-        #pragma unroll kUnrollM
-        for (int p = 0; p < M; ++p) {
-          const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
-          const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
-          cfma(acc, STAGED ? fs(Fc, i, p, j, kd) : F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
-          cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(r0, blk, p, j, kd), sf);
+        if constexpr (PC) {
+          acc = phic(kd, 2 + T + k, idx);  // includes 2 Gu_k
+        } else {
+          for (int p = 0; p < M; ++p) {
+            const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
+            const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
+            cfma(acc, STAGED ? fs(Fc, i, p, j, kd) : F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
+            cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(r0, blk, p, j, kd), sf);
+          }
+          acc += 2.f * Gu[k * NN + idx];
         }
-        acc += 2.f * Gu[k * NN + idx];
         const cf pr = Binv[j * N + i] * acc;
         v[0] += pr.re;
         v[1] += pr.im;
@@ -897,7 +1129,6 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
       const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
       const size_t row = (size_t)b * N + i;
       cf acc{0.f, 0.f};
-      #pragma unroll 8
       for (int p = 0; p < M; ++p) cfma(acc, F.at(row, blk, p, j, k), E0[i * M + p]);
       A[i * lda + j] = acc;
       if (lda > N) A[i * lda + N + j] = cf{i == j ? 1.f : 0.f, 0.f};
@@ -982,8 +1213,25 @@ void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStrea
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s) {
   const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2) * sizeof(float);
-  hipLaunchKernelGGL(det_value_kernel, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N,
-                     d.n_up, d.M, d.K);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M,
+                       d.K);
+  };
+  const int mgv = (d.M + 64 / d.N - 1) / (64 / d.N);  // harmonics per lane
+  if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
+    go(det_value_kernel<0>);
+  else if (mgv <= 4)
+    go(det_value_kernel<4>);
+  else if (mgv <= 8)
+    go(det_value_kernel<8>);
+  else if (mgv <= 16)
+    go(det_value_kernel<16>);
+  else if (mgv <= 24)
+    go(det_value_kernel<24>);
+  else if (mgv <= 32)
+    go(det_value_kernel<32>);
+  else
+    go(det_value_kernel<64>);
 }
 
 void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
@@ -995,8 +1243,20 @@ void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* 
                      d.n_up, d.M, d.K, d.orb_cols);
 }
 
+bool det_precontract(const Dims& d) {
+  static const int mode = [] {  // DH_DET_PC=0 / 1 forces the direct / precontracted form
+    const char* e = std::getenv("DH_DET_PC");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  const bool fits = 2 * d.K * d.N <= d.D && d.N <= 32 && d.M <= 16 * 4 * (64 / d.N);
+  if (mode >= 0) return fits && mode == 1;
+  // the direct kernel stages small channel rows through LDS (C2: 0.64 ms against 0.93 ms
+  // precontracted); larger rows (C4: 3.96 -> 1.92 ms, C5: 52 -> 15.5 ms) go through PhiC
+  return fits && !(det_staged(d.N, d.M, d.K) && 2 * d.M * d.N * d.K * d.N <= 8 * 256);
+}
+
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
-                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s) {
+                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic) {
   const int threads = 256;
   const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64);
   const size_t bytes = (size_t)L.total * sizeof(float);
@@ -1004,9 +1264,29 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
   auto go = [&](auto kern) {
     ensure_smem(kern, bytes);
     hipLaunchKernelGGL(kern, dim3(nw), dim3(threads), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N,
-                       d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction);
+                       d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction, (const float*)phic);
   };
-  if (!det_staged(d.N, d.M, d.K))
+  if (phic) {
+    const int mg = (d.M + 4 * (64 / d.N) - 1) / (4 * (64 / d.N));  // harmonics per lane
+    auto env = [&](auto kern, int MG) {
+      const size_t eb = env_contract_smem(d.N, d.M, MG);
+      ensure_smem(kern, eb);
+      hipLaunchKernelGGL(kern, dim3(nw * d.N), dim3(256), eb, s, F, d.ld_orb, x, geo, norm, phic, nw, d.N, d.n_up,
+                         d.M, d.K, d.Q);
+    };
+    switch (mg) {
+      case 1: env(env_contract_kernel<1>, 1); break;
+      case 2: env(env_contract_kernel<2>, 2); break;
+      case 3: env(env_contract_kernel<3>, 3); break;
+      case 4: env(env_contract_kernel<4>, 4); break;
+      case 5: env(env_contract_kernel<5>, 5); break;
+      case 6: env(env_contract_kernel<6>, 6); break;
+      case 7:
+      case 8: env(env_contract_kernel<8>, 8); break;
+      default: env(env_contract_kernel<16>, 16); break;
+    }
+    go(det_energy_kernel<0, true>);
+  } else if (!det_staged(d.N, d.M, d.K))
     go(det_energy_kernel<0>);
   else if (nrw <= 8 * threads)
     go(det_energy_kernel<8>);

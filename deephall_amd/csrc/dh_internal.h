@@ -143,8 +143,11 @@ void launch_layernorm(const Dims& d, const float* X, const float* Z, const float
 //   energy mode (C == 2N+5): e_l[nw][2], obs[nw][8]
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s);
+// phic != nullptr (det_precontract(d)): the channel matrices are first contracted from F by
+// env_contract_kernel into phic [nw][K][C][N][N] complex, then assembled from there
+bool det_precontract(const Dims& d);
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
-                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s);
+                       const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic);
 size_t det_energy_smem_bytes(const Dims& d);
 void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStream_t s);
 // mcmc.hip: accept/reject (mcmc.py:55-62).
