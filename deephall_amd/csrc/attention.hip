@@ -1067,7 +1067,7 @@ void launch_ch(const Dims& d, const float* qkv, const float* geo, float* o, int 
 // C4 / C5 configs (one wave per (walker, head) there too: 2x / 10x faster than the
 // 256-thread channel kernel v2, whose three barriers per channel dominate)
 bool attention_takes_features(const Dims& d, int C) {
-  if (C > 1 && attention_mfma_supported(d)) return false;  // the MFMA kernel reads q|k|v rows
+  (void)C;  // the wave kernels and the MFMA kernel both form layer 1's q|k|v from the features
   return d.dh == 64 && (d.N <= 8 || d.N == 10 || d.N == 20);
 }
 
@@ -1076,7 +1076,7 @@ void launch_attention(const Dims& d, const float* qkv, const float* geo, float* 
   // wave kernels (value and channel) for dh = 64, N <= 8; W0qkv != nullptr selects the
   // fused layer-1 form (q|k|v from the input features), valid only for those kernels.
   if (C > 1 && attention_mfma_supported(d)) {
-    launch_attention_mfma(d, qkv, geo, o, nw, s);
+    launch_attention_mfma(d, qkv, geo, o, nw, s, W0qkv, bqkv);
     return;
   }
   if (attention_takes_features(d, C)) {

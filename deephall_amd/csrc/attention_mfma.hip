@@ -55,10 +55,30 @@ struct MAttn {
   static constexpr int oSP = oAU + N * LDA, oAL = oSP + SPSZ, TOTAL = oAL + 3 * T;
 };
 
-template <int N>
+// Input-feature channel c of electron i (layer 1, FEAT): [z, x, y, spin] of psiformer.py:51-60
+// and their channel seeds (input.hip), from the geometry g = (st, ct, sp, cp).
+template <int T>
+__device__ __forceinline__ f4v feat_channel(int c, int i, float4 g, float spin) {
+  const float st = g.x, ct = g.y, sp = g.z, cp = g.w;
+  if (c == 0) return f4v{ct, st * cp, st * sp, spin};
+  if (c <= T) {
+    const int t = c - 1;
+    if ((t >> 1) != i) return f4v{0.f, 0.f, 0.f, 0.f};
+    return ((t & 1) == 0) ? f4v{-st, ct * cp, ct * sp, 0.f} : f4v{0.f, -sp, cp, 0.f};
+  }
+  const float rz = ct, rx = st * cp, ry = st * sp;
+  if (c == T + 1) return f4v{-2.f * rz, -2.f * rx, -2.f * ry, 0.f};
+  const int k = c - T - 2;  // rotation flow about axis k (0:x 1:y 2:z)
+  return f4v{(k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f};
+}
+
+// FEAT (layer 1): the q|k|v rows are formed from the K = 4 input features and the folded
+// W0 Wqkv (+ the bias on the value channel) in the prefetch, instead of read from memory.
+template <int N, bool FEAT>
 __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ qkv,
                                                              const float* __restrict__ geo, float* __restrict__ o,
-                                                             int H) {
+                                                             int H, const float* __restrict__ W0qkv,
+                                                             const float* __restrict__ bqkv, int n_up) {
   using L = MAttn<N>;
   constexpr int NB = L::NB, NP = L::NP, LD = L::LD, LDA = L::LDA, T = L::T, C = L::C, KQ = L::KQ, JU = L::JU,
                 NU = L::NU, NSLOT = L::NSLOT;
@@ -96,7 +116,23 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
       const int idx = tid + 256 * u;
       if (idx < 3 * N * 16) {
         const int m = idx / (N * 16), rem = idx - m * (N * 16), i = rem >> 4, q4 = rem & 15;
-        pf[u] = src[((((size_t)(b * N + i) * C + c) * 3 * D) + m * D + h * 64) / 4 + q4];
+        if constexpr (FEAT) {
+          const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+          const f4v f = feat_channel<T>(c, i, g, i < n_up ? 1.f : -1.f);
+          const int col = m * D + h * 64 + 4 * q4;
+          f4v v = {0.f, 0.f, 0.f, 0.f};
+          if (f[0] != 0.f || f[1] != 0.f || f[2] != 0.f || f[3] != 0.f) {
+            const f4v* W = reinterpret_cast<const f4v*>(W0qkv + col);
+            const f4v w0 = W[0], w1 = W[3 * D / 4], w2 = W[6 * D / 4], w3 = W[9 * D / 4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)  // the wave kernels' order: f.x w.x + (f.y w.y + (f.z w.z + f.w w.w))
+              v[e] = fmaf(f[0], w0[e], fmaf(f[1], w1[e], fmaf(f[2], w2[e], f[3] * w3[e])));
+          }
+          if (c == 0) v += *reinterpret_cast<const f4v*>(bqkv + col);
+          pf[u] = v;
+        } else {
+          pf[u] = src[((((size_t)(b * N + i) * C + c) * 3 * D) + m * D + h * 64) / 4 + q4];
+        }
       }
     }
   };
@@ -390,10 +426,17 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
 }
 
 template <int N>
-void launch_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s) {
+void launch_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s,
+                 const float* W0qkv, const float* bqkv) {
   const size_t smem = (size_t)MAttn<N>::TOTAL * sizeof(float);
-  ensure_smem(attention_mfma_kernel<N>, smem);
-  hipLaunchKernelGGL(attention_mfma_kernel<N>, dim3(nw * d.H), dim3(256), smem, s, qkv, geo, o, d.H);
+  auto go = [&](auto kern) {
+    ensure_smem(kern, smem);
+    hipLaunchKernelGGL(kern, dim3(nw * d.H), dim3(256), smem, s, qkv, geo, o, d.H, W0qkv, bqkv, d.n_up);
+  };
+  if (W0qkv)
+    go(attention_mfma_kernel<N, true>);
+  else
+    go(attention_mfma_kernel<N, false>);
 }
 
 }  // namespace
@@ -407,10 +450,11 @@ bool attention_mfma_supported(const Dims& d) {
   return on && d.dh == 64 && (d.N == 10 || d.N == 20);
 }
 
-void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s) {
+void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s,
+                           const float* W0qkv, const float* bqkv) {
   switch (d.N) {
-    case 10: launch_mfma<10>(d, qkv, geo, o, nw, s); return;
-    default: launch_mfma<20>(d, qkv, geo, o, nw, s); return;
+    case 10: launch_mfma<10>(d, qkv, geo, o, nw, s, W0qkv, bqkv); return;
+    default: launch_mfma<20>(d, qkv, geo, o, nw, s, W0qkv, bqkv); return;
   }
 }
 

@@ -128,7 +128,8 @@ void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t
 bool attention_takes_features(const Dims& d, int C);
 // channel attention on the matrix cores (attention_mfma.hip): C > 1, dh = 64, N = 10, 20
 bool attention_mfma_supported(const Dims& d);
-void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s);
+void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s,
+                           const float* W0qkv, const float* bqkv);
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
                       const float* W0qkv = nullptr, const float* bqkv = nullptr);
 
