@@ -999,7 +999,11 @@ void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
 // transposes through its own LDS region (not the ring) and its 4*TN dwordx4 stores stay
 // in flight under the next steps (counted: vmcnt(4*TN) at the next step's wait; VMEM ops of
 // a wave complete in order).  LDS: ring 3 x 40 KiB + 8 x 4.5 KiB transpose = 156 KiB.
-template <int TN, bool HAS_R>
+// R4: a 4-stage ring (160 KiB, two stages in flight instead of one: the DMA latency cover
+// doubles).  No LDS is left for a transpose region, so a tile's last step does not issue
+// its step + 3 DMA: the epilogue transposes through that free stage buffer, and the next
+// step issues two stages (its wait then counts the epilogue's stores instead).
+template <int TN, bool HAS_R, bool R4 = false, int ABLQ = 0>  // ABLQ 1: no epilogue stores (tools only)
 __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__ X, int ldx,
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
@@ -1011,6 +1015,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
   constexpr int NST = 4 * TN, TS = 36;  // stores per wave per tile; transpose row stride (floats)
   static_assert(A_BYTES % 1024 == 0 && (3 * B_PLANE) % 1024 == 0, "DMA pieces");
   static_assert(PER + NST <= 63, "vmcnt range");
+  constexpr int NS = R4 ? 4 : 3;  // ring stages
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1070,7 +1075,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
   const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
   const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
   const int boff = A_BYTES + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
-  float* red = reinterpret_cast<float*>(smem + 3 * STAGE) + wid * (32 * TS);
+  float* red = reinterpret_cast<float*>(smem + 3 * STAGE) + wid * (32 * TS);  // R4: set per tile
   const int lr = lane >> 3, lc = (lane & 7) * 4;  // read-back: rows 8q + lr, columns lc..lc+3
 
   f32x16 acc[TN];
@@ -1081,7 +1086,10 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
 
   stage(0, 0);
   if (F > 1) stage(1, 1);
-  if (F > 1)
+  if (R4 && F > 2) stage(2, 2);
+  if (R4 && F > 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PER) : "memory");
+  else if (F > 1)
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
   else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1094,20 +1102,42 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
   }
   int bcur = 0, kt = 0, tile = 0;
   bool stored = false;  // epilogue stores issued in the previous step
+  bool deferred = false;  // R4: the previous (tile-end) step left its step + 3 DMA to this one
   for (int f = 0; f < F; ++f) {
-    // wait for step f+1's DMA (issued one step ago); younger: the previous epilogue's stores
-    if (stored)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NST) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wait for step f+1's DMA; younger: (ST 3) the previous epilogue's stores, (R4) step
+    // f+2's DMA, or, after a tile end, the epilogue's stores
+    if constexpr (R4) {
+      if (deferred && stored)  // exactly NST stores behind step f+1's DMA
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NST) : "memory");
+      else if (deferred)  // a partial tile's guarded stores: drain
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (f + 2 < F)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (stored)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NST) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     stored = false;
-    int bn1 = bcur + 1, bn2 = bcur + 2;
-    if (bn1 >= 3) bn1 -= 3;
-    if (bn2 >= 3) bn2 -= 3;
-    if (f + 2 < F) stage(f + 2, bn2);
+    int bn1 = bcur + 1, bn2 = bcur + 2, bn3 = bcur + 3;
+    if (bn1 >= NS) bn1 -= NS;
+    if (bn2 >= NS) bn2 -= NS;
+    if (bn3 >= NS) bn3 -= NS;
+    const bool tile_end = kt + 1 == nk;
+    if constexpr (R4) {
+      if (deferred && f + 2 < F) stage(f + 2, bn2);  // the transpose buffer of the last epilogue
+      if (!tile_end && f + 3 < F) stage(f + 3, bn3);  // the buffer step f-1 read
+      deferred = tile_end;
+      if (tile_end) red = reinterpret_cast<float*>(smem + bn3 * STAGE) + wid * (32 * TS);
+    } else {
+      if (f + 2 < F) stage(f + 2, bn2);
+    }
     const bool more = f + 1 < F;
     float4 u, v;
     if (more) {
@@ -1203,7 +1233,8 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
             val.z += rcur[q].z;
             val.w += rcur[q].w;
           }
-          *reinterpret_cast<float4*>(Y + (size_t)(rw0 + rr) * ldy + col0 + 32 * j + lc) = val;
+          if (ABLQ == 0 || val.x == 1.2345e-30f)
+            *reinterpret_cast<float4*>(Y + (size_t)(rw0 + rr) * ldy + col0 + 32 * j + lc) = val;
         }
         if (HAS_R) {
 #pragma unroll
@@ -1235,26 +1266,28 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
     }
     // full tiles issue exactly NST stores per wave (the count the next wait assumes);
     // partial tiles drain everything at the next wait
-    stored = full;
+    stored = full && ABLQ == 0;
   }
 }
 
-template <int TN>
+template <int TN, bool R4 = false, int ABLQ = 0>
 void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
                   float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   constexpr int BM = 256, BN = 32 * TN;
   const int ntm = (rows + BM - 1) / BM, ntn = (ncols + BN - 1) / BN;
-  const size_t smem = 3ull * (BM * 16 * 4 + 3 * BN * 16 * 2) + 8ull * 32 * 36 * 4;
+  const size_t st = BM * 16 * 4 + 3 * BN * 16 * 2;
+  const size_t smem = R4 ? 4ull * st : 3ull * st + 8ull * 32 * 36 * 4;
+  static_assert(!R4 || BM * 16 * 4 + 3 * BN * 16 * 2 >= 8 * 32 * 36 * 4, "transpose fits a stage");
   int grid = std::min(ntm * ntn, cu_count_x6());
   grid = std::max(8, grid / 8 * 8);
   if (R) {
-    ensure_smem(gemm_x6q_kernel<TN, true>, smem);
-    hipLaunchKernelGGL((gemm_x6q_kernel<TN, true>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
-                       ldy, rows, ncols, K, C, ntm, ntn);
+    ensure_smem(gemm_x6q_kernel<TN, true, R4, ABLQ>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, true, R4, ABLQ>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R,
+                       ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
   } else {
-    ensure_smem(gemm_x6q_kernel<TN, false>, smem);
-    hipLaunchKernelGGL((gemm_x6q_kernel<TN, false>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R, ldr, Y,
-                       ldy, rows, ncols, K, C, ntm, ntn);
+    ensure_smem(gemm_x6q_kernel<TN, false, R4, ABLQ>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, false, R4, ABLQ>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias,
+                       R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
   }
 }
 
@@ -1561,6 +1594,14 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
     case 52:
       launch_x6q_t<4>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
+    // persistent lean, 4-stage ring (two stages in flight)
+    case 53:
+      launch_x6q_t<8, true>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 95:  // ablation of 50: no epilogue stores (wrong results; tools/gemm_bench.py only)
+      launch_x6q_t<8, false, 1>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+
     // ablations of variant 40 (wrong results; tools/gemm_bench.py only)
     case 91:
       launch_x6d_t<8, 1>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
