@@ -47,6 +47,8 @@ EXPORTS = [
     "dh_loss_diff",
     "dh_init_walkers",
     "dh_potential",
+    "dh_histograms",
+    "dh_monopole_orbitals",
     "dh_debug_trunk",
     "dh_debug_gemm",
     "dh_debug_gemm_ln",
@@ -134,6 +136,10 @@ def load(path: Path | str | None = None):
     lib.dh_init_walkers.restype = i32
     lib.dh_potential.argtypes = [vp, vp, i32, vp, vp]
     lib.dh_potential.restype = i32
+    lib.dh_histograms.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp]
+    lib.dh_histograms.restype = i32
+    lib.dh_monopole_orbitals.argtypes = [vp, i32, i32, vp, vp]
+    lib.dh_monopole_orbitals.restype = i32
     lib.dh_debug_trunk.argtypes = [vp, vp, i32, i32, vp, sz, vp]
     lib.dh_debug_trunk.restype = i32
     lib.dh_debug_f_offset.argtypes = [vp, i32, i32]

@@ -1109,6 +1109,21 @@ int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream) {
   return check_launch();
 }
 
+int dh_histograms(const float* x, int B, int nelec, int density_bins, int pair_bins, float* density, float* pair,
+                  void* stream) {
+  if (!x || B < 1 || nelec < 1 || density_bins < 0 || pair_bins < 0 || density_bins + pair_bins < 1 ||
+      density_bins + pair_bins > 8192 || (density_bins && !density) || (pair_bins && !pair))
+    return fail(DH_EINVAL, "bad arguments");
+  launch_histograms(x, B, nelec, density_bins, pair_bins, density, pair, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_monopole_orbitals(const float* points, int n, int flux, float* out, void* stream) {
+  if (!points || !out || n < 1 || flux < 0 || flux > 126) return fail(DH_EINVAL, "bad arguments");
+  launch_monopole_orbitals(points, n, flux, out, (hipStream_t)stream);
+  return check_launch();
+}
+
 int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream) {
   if (!h || !x || B < 1) return fail(DH_EINVAL, "bad arguments");
   launch_init_walkers(h->d, x, B, seed, walker_offset, (hipStream_t)stream);

@@ -146,6 +146,9 @@ void launch_det_value(const Dims& d, const float* F, const float* x, const float
                       float* logpsi, int nw, hipStream_t s);
 // phic != nullptr (det_precontract(d)): the channel matrices are first contracted from F by
 // env_contract_kernel into phic [nw][K][C][N][N] complex, then assembled from there
+// NetObs estimators (netobs.hip): theta / pair-angle histograms, LLL monopole harmonics
+void launch_histograms(const float* x, int B, int N, int db, int pb, float* dens, float* pair, hipStream_t s);
+void launch_monopole_orbitals(const float* pts, int n, int flux, float* out, hipStream_t s);
 bool det_precontract(const Dims& d);
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic);

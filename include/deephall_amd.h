@@ -231,6 +231,19 @@ int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const 
  * interaction_strength: pe[B]. */
 int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream);
 
+/* ---- NetObs-style estimators (deephall/netobs_bridge/observables/*.py) ----------------
+ * dh_histograms ADDS to density[density_bins] the counts of every electron's theta and
+ * to pair[pair_bins] the 1/sin(theta_12)-weighted counts of every pair angle
+ * theta_12 = arccos(r_i . r_j), i < j, both over [0, pi] with numpy's bin rule
+ * (density.py:38-44, pair_corr.py:43-58; the caller applies pair_corr.py:57's scale).
+ * Either count may be 0 (its pointer then unused).  Walkers x[B][nelec][2]. */
+int dh_histograms(const float* x, int B, int nelec, int density_bins, int pair_bins, float* density, float* pair,
+                  void* stream);
+/* Lowest-Landau-level monopole harmonics Y_{Q,Q,m}, m = -Q..Q, Q = flux / 2, at n points
+ * (theta, phi): out[n][flux + 1] complex (re, im), one_rdm.py:31-54 (cos theta clipped to
+ * +-(1 - 1e-4) as there). */
+int dh_monopole_orbitals(const float* points, int n, int flux, float* out, void* stream);
+
 /* Kernel timing with HIP events on the launch stream (bench / roofline).
  * dh_profile_enable(h, 1) starts recording every kernel launch of this handle;
  * dh_profile_read fills out[k*4 + {0,1,2,3}] = {launches, total ms, algorithmic
