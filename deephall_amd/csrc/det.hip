@@ -304,7 +304,10 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
 // LDS-DMA ring depth: up to 4 rows, (depth - 1) rows of 2 MG loads within vmcnt's 6 bits
 __host__ __device__ constexpr int env_ring(int MG) { return (63 / (2 * MG) + 1) < 4 ? (63 / (2 * MG) + 1) : 4; }
 
-template <int MG>
+// WU (short rows, C4): one WAVE per (walker, electron) instead of one workgroup: no
+// cross-wave partials, no block barriers, 4 units per workgroup (the leaves of a unit are
+// computed by its own 64 lanes).
+template <int MG, bool WU = false>
 __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restrict__ Fp, int ldF,
                                                            const float* __restrict__ x,
                                                            const float* __restrict__ geo_g,
@@ -314,12 +317,17 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   static_assert((RING - 1) * Q2 <= 63, "vmcnt range");
   extern __shared__ float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int b = blockIdx.x / N, i = blockIdx.x - (blockIdx.x / N) * N;
+  const int unit = WU ? blockIdx.x * 4 + wv : blockIdx.x;
+  if (WU && unit >= nw * N) return;  // whole waves only (no block barriers in the WU form)
+  const int b = unit / N, i = unit - (unit / N) * N;
   const int T = 2 * N, C = 2 * N + 5;
-  cf* wt = reinterpret_cast<cf*>(sm);         // [E0, DTH, DPH, LB, W0..2, SF0..2][M]
-  cf* part = wt + 10 * M;                     // [4 waves][C][N] partial sums
-  float* al = reinterpret_cast<float*>(part + 4 * C * N);  // [3][T]
-  float* ring = al + ((3 * T + 3) & ~3);      // [4 waves][RING][Q2][64]
+  // LDS: WU: per wave [wt | al | ring]; else [wt | part | al | 4 rings]
+  const int wsz = WU ? 20 * M + ((3 * T + 3) & ~3) + RING * Q2 * 64 : 0;
+  cf* wt = reinterpret_cast<cf*>(sm + (size_t)wv * wsz);  // [E0, DTH, DPH, LB, W0..2, SF0..2][M]
+  cf* part = wt + 10 * M;                                 // [4 waves][C][N] partial sums (not WU)
+  float* al = reinterpret_cast<float*>(WU ? part : part + 4 * C * N);  // [3][T]
+  float* ring = al + ((3 * T + 3) & ~3);                  // [RING][Q2][64] per wave
+  const int lt = WU ? lane : tid, nlt = WU ? 64 : 256;    // threads computing the leaves
   {
     const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
     const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
     const float th = x[2 * (b * N + i)], ph = x[2 * (b * N + i) + 1];
     const float phh[3] = {-sp, cp, 0.f};
     const float thh[3] = {ct * cp, ct * sp, -st};
-    for (int p = tid; p < M; p += 256) {
+    for (int p = lt; p < M; p += nlt) {
       const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge);
       wt[p] = e.e0;
       wt[M + p] = e.dth;
@@ -340,16 +348,19 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
         wt[(7 + k) * M + p] = env_flow2(e.e0, e.dth, e.d2th, mf, st, ct, sp, cp, k);
       }
     }
-    if (tid < T) {  // alpha_kt from the geometry of the electron tangent t moves
-      const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (tid >> 1)));
-      al[tid] = (tid & 1) ? -(ga.y * ga.w) : -ga.z;
-      al[T + tid] = (tid & 1) ? -(ga.y * ga.z) : ga.w;
-      al[2 * T + tid] = (tid & 1) ? ga.x : 0.f;
+    if (lt < T) {  // alpha_kt from the geometry of the electron tangent t moves
+      const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (lt >> 1)));
+      al[lt] = (lt & 1) ? -(ga.y * ga.w) : -ga.z;
+      al[T + lt] = (lt & 1) ? -(ga.y * ga.z) : ga.w;
+      al[2 * T + lt] = (lt & 1) ? ga.x : 0.f;
     }
   }
-  __syncthreads();
-  const int G = 64 / N, j = lane % N, g = lane / N, S = 4 * G;
-  const int gg = G * wv + g;
+  if constexpr (WU)
+    __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+  else
+    __syncthreads();
+  const int G = 64 / N, j = lane % N, g = lane / N, S = WU ? G : 4 * G;
+  const int gg = WU ? g : G * wv + g;
   const bool act = g < G;
   const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
   const int NK = N * K, MNK = M * NK;
@@ -363,7 +374,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   // lane's harmonic u (< MG) is m = gg + S u, valid when m < M (and g < G)
   auto mw = [&](int u) __attribute__((always_inline)) { return min(gg + S * u, M - 1); };
   auto okm = [&](int u) __attribute__((always_inline)) { return act && gg + S * u < M; };
-  float* wring = ring + (size_t)wv * RING * Q2 * 64;
+  float* wring = WU ? ring : ring + (size_t)wv * RING * Q2 * 64;
   const uint32_t ring0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)wring);
   // DMA row c of det kd into ring slot c % RING
   auto issue = [&](int c, int kd) __attribute__((always_inline)) {
@@ -457,8 +468,17 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
         }
       }
       const cf v = gsumc(e0a);
-      if (g == 0) part[((size_t)wv * C + c) * N + j] = v;
+      if constexpr (WU) {
+        if (g == 0) {
+          float* o = PhiC + 2 * (((size_t)(b * K + kd) * C + c) * N * N + (size_t)i * N + j);
+          o[0] = v.re;
+          o[1] = v.im;
+        }
+      } else {
+        if (g == 0) part[((size_t)wv * C + c) * N + j] = v;
+      }
     }
+    if constexpr (WU) continue;
     __syncthreads();
     float* out = PhiC + 2 * ((size_t)(b * K + kd) * C * N * N + (size_t)i * N);
     for (int e = tid; e < C * N; e += 256) {
@@ -471,9 +491,10 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   }
 }
 
-// dynamic LDS of env_contract_kernel<MG>
-size_t env_contract_smem(int N, int M, int MG) {
+// dynamic LDS of env_contract_kernel<MG, WU>
+size_t env_contract_smem(int N, int M, int MG, bool WU) {
   const int T = 2 * N, C = 2 * N + 5;
+  if (WU) return (size_t)4 * (20 * M + ((3 * T + 3) & ~3) + env_ring(MG) * 2 * MG * 64) * sizeof(float);
   return (size_t)(20 * M + 8 * C * N + ((3 * T + 3) & ~3) + 4 * env_ring(MG) * 2 * MG * 64) * sizeof(float);
 }
 
@@ -1267,23 +1288,35 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
                        d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction, (const float*)phic);
   };
   if (phic) {
-    const int mg = (d.M + 4 * (64 / d.N) - 1) / (4 * (64 / d.N));  // harmonics per lane
-    auto env = [&](auto kern, int MG) {
-      const size_t eb = env_contract_smem(d.N, d.M, MG);
+    const int G = 64 / d.N;
+    const int mgw = (d.M + G - 1) / G;          // harmonics per lane, one wave per electron
+    const int mg = (d.M + 4 * G - 1) / (4 * G);  // harmonics per lane, four waves per electron
+    auto env = [&](auto kern, int MG, bool WU) {
+      const size_t eb = env_contract_smem(d.N, d.M, MG, WU);
       ensure_smem(kern, eb);
-      hipLaunchKernelGGL(kern, dim3(nw * d.N), dim3(256), eb, s, F, d.ld_orb, x, geo, norm, phic, nw, d.N, d.n_up,
-                         d.M, d.K, d.Q);
+      const int grid = WU ? (nw * d.N + 3) / 4 : nw * d.N;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), eb, s, F, d.ld_orb, x, geo, norm, phic, nw, d.N, d.n_up, d.M,
+                         d.K, d.Q);
     };
-    switch (mg) {
-      case 1: env(env_contract_kernel<1>, 1); break;
-      case 2: env(env_contract_kernel<2>, 2); break;
-      case 3: env(env_contract_kernel<3>, 3); break;
-      case 4: env(env_contract_kernel<4>, 4); break;
-      case 5: env(env_contract_kernel<5>, 5); break;
-      case 6: env(env_contract_kernel<6>, 6); break;
-      case 7:
-      case 8: env(env_contract_kernel<8>, 8); break;
-      default: env(env_contract_kernel<16>, 16); break;
+    if (mgw <= 4) {  // short rows (C4: M = 24, N = 10): a wave per electron
+      switch (mgw) {
+        case 1: env(env_contract_kernel<1, true>, 1, true); break;
+        case 2: env(env_contract_kernel<2, true>, 2, true); break;
+        case 3: env(env_contract_kernel<3, true>, 3, true); break;
+        default: env(env_contract_kernel<4, true>, 4, true); break;
+      }
+    } else {
+      switch (mg) {
+        case 1: env(env_contract_kernel<1>, 1, false); break;
+        case 2: env(env_contract_kernel<2>, 2, false); break;
+        case 3: env(env_contract_kernel<3>, 3, false); break;
+        case 4: env(env_contract_kernel<4>, 4, false); break;
+        case 5: env(env_contract_kernel<5>, 5, false); break;
+        case 6: env(env_contract_kernel<6>, 6, false); break;
+        case 7:
+        case 8: env(env_contract_kernel<8>, 8, false); break;
+        default: env(env_contract_kernel<16>, 16, false); break;
+      }
     }
     go(det_energy_kernel<0, true>);
   } else if (!det_staged(d.N, d.M, d.K))

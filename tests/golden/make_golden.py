@@ -142,7 +142,7 @@ def round2():
     energy_case("C2_harmonic_radius", "C2", 16, seed=35, interaction_type="harmonic", radius=2.5)
     energy_case("C2_radius", "C2", 16, seed=36, radius=3.1)
     energy_case("C2", "C2", 32, seed=37)
-    energy_case("C4", "C4", 32, seed=38)
+    energy_case("C4", "C4", 128, seed=38)  # 128 walkers: the p90 of a 32-walker batch is its 4th-worst walker
     energy_case("C5", "C5", 32, seed=39)
     mcmc_case("C4", B=16, steps=3)
 
