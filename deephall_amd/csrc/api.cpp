@@ -48,7 +48,7 @@ struct Work {
 
 Work carve(const Dims& d, int nw, int C, void* base) {
   const int rows = nw * d.N * C;
-  const size_t rp = (size_t)round_up(std::max(rows, 1), kRowPad);
+  const size_t rp = (size_t)round_up(std::max(rows, 1), kWalkerRowPad);
   const size_t nh = align64(rp * d.D);
   const size_t nqkv = align64(rp * (size_t)std::max(3 * d.D, d.ld_orb));
   Work w{};

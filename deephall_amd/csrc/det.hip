@@ -327,38 +327,6 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   cf* part = wt + 10 * M;                                 // [4 waves][C][N] partial sums (not WU)
   float* al = reinterpret_cast<float*>(WU ? part : part + 4 * C * N);  // [3][T]
   float* ring = al + ((3 * T + 3) & ~3);                  // [RING][Q2][64] per wave
-  const int lt = WU ? lane : tid, nlt = WU ? 64 : 256;    // threads computing the leaves
-  {
-    const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
-    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
-    const float gauge = ct >= 0.f ? Q : -Q;
-    const float th = x[2 * (b * N + i)], ph = x[2 * (b * N + i) + 1];
-    const float phh[3] = {-sp, cp, 0.f};
-    const float thh[3] = {ct * cp, ct * sp, -st};
-    for (int p = lt; p < M; p += nlt) {
-      const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge);
-      wt[p] = e.e0;
-      wt[M + p] = e.dth;
-      wt[2 * M + p] = e.dph;
-      wt[3 * M + p] = e.lb;
-      const float mf = (float)p - 0.5f * (float)(M - 1) - gauge;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        wt[(4 + k) * M + p] = cf{phh[k] * e.dth.re - thh[k] * e.dph.re, phh[k] * e.dth.im - thh[k] * e.dph.im};
-        wt[(7 + k) * M + p] = env_flow2(e.e0, e.dth, e.d2th, mf, st, ct, sp, cp, k);
-      }
-    }
-    if (lt < T) {  // alpha_kt from the geometry of the electron tangent t moves
-      const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (lt >> 1)));
-      al[lt] = (lt & 1) ? -(ga.y * ga.w) : -ga.z;
-      al[T + lt] = (lt & 1) ? -(ga.y * ga.z) : ga.w;
-      al[2 * T + lt] = (lt & 1) ? ga.x : 0.f;
-    }
-  }
-  if constexpr (WU)
-    __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
-  else
-    __syncthreads();
   const int G = 64 / N, j = lane % N, g = lane / N, S = WU ? G : 4 * G;
   const int gg = WU ? g : G * wv + g;
   const bool act = g < G;
@@ -416,10 +384,54 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
     const float* r = wring + (size_t)((c % RING) * Q2 + 2 * u) * 64 + lane;
     return okm(u) ? cf{r[0], r[64]} : cf{0.f, 0.f};
   };
+  // the first rows' DMA goes out before the envelope leaves are computed (it does not need
+  // them); the leaves' few global operands are loaded (and waited for) first, so no
+  // compiler-inserted wait inside the leaves drains the DMA queue
+  const int lt = WU ? lane : tid, nlt = WU ? 64 : 256;  // threads computing the leaves
+  const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
+  const float th = x[2 * (b * N + i)], ph = x[2 * (b * N + i) + 1];
+  const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (lt < T ? lt >> 1 : 0)));
+  float nrm[2];  // norm of this thread's harmonics (M <= 2 nlt)
+  nrm[0] = lt < M ? norm[lt] : 0.f;
+  nrm[1] = lt + nlt < M ? norm[lt + nlt] : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int c = 0; c < RING - 1 && c < C; ++c) issue(c, 0);
+  {
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const float gauge = ct >= 0.f ? Q : -Q;
+    const float phh[3] = {-sp, cp, 0.f};
+    const float thh[3] = {ct * cp, ct * sp, -st};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int p = lt + r * nlt;
+      if (p >= M) break;
+      const EnvLeaf e = env_leaf(th, ph, p, M, nrm[r], true, gauge);
+      wt[p] = e.e0;
+      wt[M + p] = e.dth;
+      wt[2 * M + p] = e.dph;
+      wt[3 * M + p] = e.lb;
+      const float mf = (float)p - 0.5f * (float)(M - 1) - gauge;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        wt[(4 + k) * M + p] = cf{phh[k] * e.dth.re - thh[k] * e.dph.re, phh[k] * e.dth.im - thh[k] * e.dph.im};
+        wt[(7 + k) * M + p] = env_flow2(e.e0, e.dth, e.d2th, mf, st, ct, sp, cp, k);
+      }
+    }
+    if (lt < T) {  // alpha_kt from the geometry of the electron tangent t moves
+      al[lt] = (lt & 1) ? -(ga.y * ga.w) : -ga.z;
+      al[T + lt] = (lt & 1) ? -(ga.y * ga.z) : ga.w;
+      al[2 * T + lt] = (lt & 1) ? ga.x : 0.f;
+    }
+  }
+  if constexpr (WU)
+    __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+  else
+    __syncthreads();
   for (int kd = 0; kd < K; ++kd) {
     cf xd{0.f, 0.f}, xp{0.f, 0.f}, xl{0.f, 0.f}, xs0{0.f, 0.f}, xs1{0.f, 0.f}, xs2{0.f, 0.f};  // F_0 extras
     cf lb2{0.f, 0.f}, gu0{0.f, 0.f}, gu1{0.f, 0.f}, gu2{0.f, 0.f};                            // lane partials
-    for (int c = 0; c < RING - 1 && c < C; ++c) issue(c, kd);
+    if (kd > 0)
+      for (int c = 0; c < RING - 1 && c < C; ++c) issue(c, kd);
     for (int c = 0; c < C; ++c) {
       if (c + RING - 1 < C) issue(c + RING - 1, kd);  // its slot's last reader was row c - 1
       wait_row(c);
@@ -1269,7 +1281,7 @@ bool det_precontract(const Dims& d) {
     const char* e = std::getenv("DH_DET_PC");
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  const bool fits = 2 * d.K * d.N <= d.D && d.N <= 32 && d.M <= 16 * 4 * (64 / d.N);
+  const bool fits = 2 * d.K * d.N <= d.D && d.N <= 32 && d.M <= 16 * 4 * (64 / d.N) && d.M <= 128;
   if (mode >= 0) return fits && mode == 1;
   // the direct kernel stages small channel rows through LDS (C2: 0.64 ms against 0.93 ms
   // precontracted); larger rows (C4: 3.96 -> 1.92 ms, C5: 52 -> 15.5 ms) go through PhiC

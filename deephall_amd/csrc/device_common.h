@@ -91,5 +91,38 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// Sum over each 16-lane row (DPP: quad swaps, then the half-row and row mirrors); every
+// lane of the row receives the sum.  VALU only: no LDS permute round trips.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+
+// tanh by the odd rational form XLA / Eigen evaluate for f32 (argument clamped to
+// +-7.90531, x itself below 4e-4; the quotient by reciprocal + one Newton step): a few ulp
+// against float64 tanh (tests/test_gpu_kernels.py), ~16 VALU operations against libm's ~40
+__device__ __forceinline__ float tanh_rat(float x) {
+  const float c = fminf(fmaxf(x, -7.90531110763549805f), 7.90531110763549805f);
+  const float x2 = c * c;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(p, x2, -8.60467152213735e-11f);
+  p = fmaf(p, x2, 5.12229709037114e-08f);
+  p = fmaf(p, x2, 1.48572235717979e-05f);
+  p = fmaf(p, x2, 6.37261928875436e-04f);
+  p = fmaf(p, x2, 4.89352455891786e-03f);
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(q, x2, 2.26843463243900e-03f);
+  q = fmaf(q, x2, 4.89352518554385e-03f);
+  float rq = __builtin_amdgcn_rcpf(q);  // q in [4.9e-3, 2.1e-2]: one Newton step
+  rq = rq * fmaf(-q, rq, 2.f);
+  return fabsf(x) < 4e-4f ? x : (c * p) * rq;
+}
 
 }  // namespace dh

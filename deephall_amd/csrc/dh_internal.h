@@ -56,6 +56,9 @@ struct Pass {
 };
 
 constexpr int kRowPad = 256;
+// walker-row buffers (h, qkv, o, t) are padded to 768 = lcm(96, 256) rows, so the log-psi
+// LayerNorm GEMM may take 64-, 96- or 128-row tiles without reading past the buffer
+constexpr int kWalkerRowPad = 768;
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).

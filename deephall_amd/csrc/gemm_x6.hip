@@ -590,6 +590,8 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
                                                        int ntn, const float* __restrict__ ln, X6Feat feat) {
   // NW x WN waves: wave (wm, wn) computes rows 32 wm.. and columns 32 TN wn.. of the tile
   constexpr int NWT = NW * WN;
+  // ablation switches (ABL 5: the full main loop, no epilogue)
+  constexpr bool A_DMA = ABL == 0 || ABL >= 5, A_SPLIT = ABL < 2 || ABL >= 5, A_LDS = ABL < 3 || ABL >= 5;
   constexpr int BM = 32 * NW, BN = 32 * TN * WN, BK = 16;
   static_assert(LNM == 0 || BN == 256, "LayerNorm epilogue needs whole 256-column rows");
   static_assert(WN == 1 || BN == 256, "shared-tile epilogue: 64 lanes x 4 columns");
@@ -717,7 +719,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   int bcur = 0;
   bf16x8 rb0 = c0, rb1 = c1, rb2 = c2;  // ABL 3 operands
   for (int kt = 0; kt < nk; ++kt) {
-    if (ABL == 0) {
+    if (A_DMA) {
       if (ST > 3 && kt + ST - 2 < nk)  // stages kt + 2 .. kt + ST - 2 issued: they may stay in flight
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"((ST > 3 ? ST - 3 : 0) * PER) : "memory");
       else
@@ -727,11 +729,11 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
     int bn1 = bcur + 1, bnl = bcur + ST - 1;
     if (bn1 >= ST) bn1 -= ST;
     if (bnl >= ST) bnl -= ST;
-    if (ABL == 0 && kt + ST - 1 < nk) stage(kt + ST - 1, bnl);
+    if (A_DMA && kt + ST - 1 < nk) stage(kt + ST - 1, bnl);
     const bool more = kt + 1 < nk;
     float4 u, v;
     if (more) {
-      if (ABL < 3) {
+      if (A_LDS) {
         const char* An = smem + bn1 * STAGE;  // ABL 3, 4: no LDS reads
         u = *reinterpret_cast<const float4*>(An + aoff0);
         v = *reinterpret_cast<const float4*>(An + aoff1);
@@ -746,7 +748,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bf16x8 b0, b1, b2;
-      if (ABL < 3) {
+      if (A_LDS) {
         b0 = *reinterpret_cast<const bf16x8*>(Bs + j * 1024);
         b1 = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + j * 1024);
         b2 = *reinterpret_cast<const bf16x8*>(Bs + 2 * B_PLANE + j * 1024);
@@ -762,7 +764,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
       if (j == TN / 2 && more) {
-        if (ABL < 2) {
+        if (A_SPLIT) {
           split3(u, v, n0, n1, n2);
         } else {
           n0 = __builtin_bit_cast(bf16x8, u);
@@ -781,7 +783,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   }
   }  // ST == 3
 
-  if (ABL >= 4) {  // ablation: no stores unless the impossible happens (keeps the MFMAs live)
+  if (ABL == 4 || ABL == 5) {  // ablation: no stores unless the impossible happens (keeps the MFMAs live)
     float t = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -796,12 +798,38 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   // through a private LDS region (row stride 68 floats: conflict-free ds_write_b128) and
   // writes whole 256-B row pieces with global_store_dwordx4 (4 rows per instruction; the
   // residual is read the same way).  dword stores of the MFMA layout were store-issue bound.
-  __syncthreads();  // every wave is done with the ring buffers
   if constexpr (LNM != 0) {
+    // 16 lanes per row, 4 rows per pass: lane (rq = lane >> 4, sub = lane & 15) owns columns
+    // c_k = 4 sub + 64 k (k < 4) of tile row 4 (wid + NWT p) + rq, so one store instruction
+    // writes four 256-B row pieces and the row statistics are 16-lane DPP sums (two-pass
+    // mean / centred variance, eps 1e-5, as gemm_ln_kernel).  The residual (h, or geo for
+    // the feature residual) of PC passes is loaded before the tile exchange, so the passes
+    // wait on no global load (R aliases Y: the compiler may not hoist the loads itself).
+    constexpr int NP = BM / (4 * NWT), PC = NP < 2 ? NP : 2;
+    static_assert(BM % (4 * NWT) == 0 && NP % PC == 0, "rows per wave");
+    const int sub = lane & 15, rq = lane >> 4;
+    float4 rpre[PC][4];
+    auto load_res = [&](int p0) {
+#pragma unroll
+      for (int pc = 0; pc < PC; ++pc) {
+        const int r = row0 + 4 * (wid + NWT * (p0 + pc)) + rq;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          rpre[pc][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (r < rows) {
+            if (feat.W0) {
+              if (k == 0) rpre[pc][0] = *reinterpret_cast<const float4*>(feat.geo + 4 * (size_t)r);
+            } else {
+              rpre[pc][k] = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + 4 * sub + 64 * k);
+            }
+          }
+        }
+      }
+    };
+    load_res(0);
+    __syncthreads();  // every wave is done with the ring buffers
     // every wave puts its 32 x 32TN block into the shared [BM][LS] tile (row stride 260:
-    // conflict-free ds_write_b128, as 68 below); then each wave normalises whole rows
-    // wid, wid + NWT, ...: 64 lanes x 4 columns, row statistics by wave reduction
-    // (two-pass mean / centred variance, eps 1e-5, as gemm_ln_kernel)
+    // conflict-free ds_write_b128, as 68 below)
     constexpr int LS = 260;
     float* blk = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -811,70 +839,93 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
         *reinterpret_cast<float4*>(blk + (32 * wm + l32) * LS + 32 * (wn * TN + j) + 8 * g + 4 * lh) =
             make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
     __syncthreads();
-    const int c = 4 * lane;
-    const float4 bv = *reinterpret_cast<const float4*>(bias + c);
-    const float4 gm = *reinterpret_cast<const float4*>(ln + c);
-    const float4 bt = *reinterpret_cast<const float4*>(ln + 256 + c);
-    float4 w0[4];  // residual from the features (feat.W0): input.hip's h = f W0, same order
-    if (feat.W0) {
+    float4 bv[4], gm[4], bt[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w0[q] = *reinterpret_cast<const float4*>(feat.W0 + q * 256 + c);
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * sub + 64 * k;
+      bv[k] = *reinterpret_cast<const float4*>(bias + c);
+      gm[k] = *reinterpret_cast<const float4*>(ln + c);
+      bt[k] = *reinterpret_cast<const float4*>(ln + 256 + c);
     }
-    auto wsum = [](float t) {
-      t += __shfl_xor(t, 1, 64);
-      t += __shfl_xor(t, 2, 64);
-      t += __shfl_xor(t, 4, 64);
-      t += __shfl_xor(t, 8, 64);
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      return t;
-    };
-    for (int rr = wid; rr < BM; rr += NWT) {
-      const int r = row0 + rr;
-      float4 v = *reinterpret_cast<const float4*>(blk + rr * LS + c);
-      v.x += bv.x;
-      v.y += bv.y;
-      v.z += bv.z;
-      v.w += bv.w;
-      if (LNM == 2) {
-        v.x = tanhf(v.x);
-        v.y = tanhf(v.y);
-        v.z = tanhf(v.z);
-        v.w = tanhf(v.w);
-      }
-      if (r < rows) {
-        float4 rv;
-        if (feat.W0) {
-          const float4 g = *reinterpret_cast<const float4*>(feat.geo + 4 * (size_t)r);  // st ct sp cp
-          const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (r % feat.N < feat.n_up) ? 1.f : -1.f);
-          rv.x = f.x * w0[0].x + f.y * w0[1].x + f.z * w0[2].x + f.w * w0[3].x;
-          rv.y = f.x * w0[0].y + f.y * w0[1].y + f.z * w0[2].y + f.w * w0[3].y;
-          rv.z = f.x * w0[0].z + f.y * w0[1].z + f.z * w0[2].z + f.w * w0[3].z;
-          rv.w = f.x * w0[0].w + f.y * w0[1].w + f.z * w0[2].w + f.w * w0[3].w;
-        } else {
-          rv = *reinterpret_cast<const float4*>(R + (size_t)r * ldr + c);
+    for (int p0 = 0; p0 < NP; p0 += PC) {
+      if (p0 > 0) load_res(p0);
+#pragma unroll
+      for (int pc = 0; pc < PC; ++pc) {
+        const int rr = 4 * (wid + NWT * (p0 + pc)) + rq;
+        const int r = row0 + rr;
+        float4 v[4];
+        float f[4];
+        if (feat.W0) {  // input.hip's h = f W0, same order
+          const float4 g = rpre[pc][0];  // st ct sp cp
+          f[0] = g.y;
+          f[1] = g.x * g.w;
+          f[2] = g.x * g.z;
+          f[3] = (r % feat.N < feat.n_up) ? 1.f : -1.f;
         }
-        v.x += rv.x;
-        v.y += rv.y;
-        v.z += rv.z;
-        v.w += rv.w;
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = 4 * sub + 64 * k;
+          float4 t = *reinterpret_cast<const float4*>(blk + rr * LS + c);
+          t.x += bv[k].x;
+          t.y += bv[k].y;
+          t.z += bv[k].z;
+          t.w += bv[k].w;
+          if (LNM == 2 && ABL != 7) {  // ABL 7: ablation, no tanh
+            t.x = tanh_rat(t.x);
+            t.y = tanh_rat(t.y);
+            t.z = tanh_rat(t.z);
+            t.w = tanh_rat(t.w);
+          }
+          if (r < rows) {
+            float4 rv;
+            if (feat.W0) {
+              float4 w0[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w0[q] = *reinterpret_cast<const float4*>(feat.W0 + q * 256 + c);
+              rv.x = f[0] * w0[0].x + f[1] * w0[1].x + f[2] * w0[2].x + f[3] * w0[3].x;
+              rv.y = f[0] * w0[0].y + f[1] * w0[1].y + f[2] * w0[2].y + f[3] * w0[3].y;
+              rv.z = f[0] * w0[0].z + f[1] * w0[1].z + f[2] * w0[2].z + f[3] * w0[3].z;
+              rv.w = f[0] * w0[0].w + f[1] * w0[1].w + f[2] * w0[2].w + f[3] * w0[3].w;
+            } else {
+              rv = rpre[pc][k];
+            }
+            t.x += rv.x;
+            t.y += rv.y;
+            t.z += rv.z;
+            t.w += rv.w;
+          }
+          v[k] = t;
+          sum += (t.x + t.y) + (t.z + t.w);
+        }
+        const float mean = (ABL == 6 ? sum : row16_sum(sum)) * (1.f / 256.f);
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k].x -= mean;
+          v[k].y -= mean;
+          v[k].z -= mean;
+          v[k].w -= mean;
+          ss += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
+        }
+        const float var = (ABL == 6 ? ss : row16_sum(ss)) * (1.f / 256.f);
+        const float rs = __builtin_amdgcn_rsqf(var + 1e-5f);
+        if (r < rows) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float4 o;
+            o.x = gm[k].x * (rs * v[k].x) + bt[k].x;
+            o.y = gm[k].y * (rs * v[k].y) + bt[k].y;
+            o.z = gm[k].z * (rs * v[k].z) + bt[k].z;
+            o.w = gm[k].w * (rs * v[k].w) + bt[k].w;
+            *reinterpret_cast<float4*>(Y + (size_t)r * ldy + 4 * sub + 64 * k) = o;
+          }
+        }
       }
-      const float mean = wsum((v.x + v.y) + (v.z + v.w)) * (1.f / 256.f);
-      v.x -= mean;
-      v.y -= mean;
-      v.z -= mean;
-      v.w -= mean;
-      const float var = wsum((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w)) * (1.f / 256.f);
-      const float rs = 1.f / sqrtf(var + 1e-5f);
-      float4 o;
-      o.x = gm.x * (rs * v.x) + bt.x;
-      o.y = gm.y * (rs * v.y) + bt.y;
-      o.z = gm.z * (rs * v.z) + bt.z;
-      o.w = gm.w * (rs * v.w) + bt.w;
-      if (r < rows) *reinterpret_cast<float4*>(Y + (size_t)r * ldy + c) = o;
     }
     return;
   }
+  __syncthreads();  // every wave is done with the ring buffers
   if constexpr (WN > 1) {
     // plain epilogue of the 2-D wave grid: the same shared tile, then whole 1-KB row
     // pieces per wave instruction (ncols % 4 == 0: a float4 is in or out as a whole)
@@ -1598,6 +1649,9 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
     case 53:
       launch_x6q_t<8, true>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
+    case 55:
+      launch_x6q_t<5>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
     case 95:  // ablation of 50: no epilogue stores (wrong results; tools/gemm_bench.py only)
       launch_x6q_t<8, false, 1>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
@@ -1627,11 +1681,26 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
   // (log-psi) row counts take 256 x 128 tiles, two workgroups per CU (128 x 192 when ncols
   // is a multiple of 192: q|k|v 24576 x 768 in 64 vs 68 us).  The 2-D wave grids (60-62)
   // were no faster at these shapes (tools/ln_gemm_bench.py).
+  // Channel rows: below 1024 columns the width with the least padding (C4's orbital map,
+  // 480 columns: 256-wide 2125 us, 192-wide 1816 us, 160-wide 1628 us; tools/gemm_orb_bench.py),
+  // else 256 (C5's 2320 columns: 12.9 ms against 13.8 ms 160-wide)
   int v;
-  if (rows >= 65536)
-    v = (ncols % 192 == 0 && ncols % 256 != 0) ? 51 : 50;
-  else
+  if (rows >= 65536) {
+    v = 50;
+    if (ncols < 1024) {
+      const int tns[4] = {8, 6, 5, 4}, vs[4] = {50, 51, 55, 52};
+      int best = round_up(ncols, 256);
+      for (int q = 1; q < 4; ++q) {
+        const int padded = round_up(ncols, 32 * tns[q]);
+        if (padded < best) {
+          best = padded;
+          v = vs[q];
+        }
+      }
+    }
+  } else {
     v = (ncols % 192 == 0) ? 44 : 46;
+  }
   launch_gemm_x6_variant(v, X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
 }
 
@@ -1639,14 +1708,49 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
 // log-psi GEMM + LayerNorm (LNM 1 / 2 above), in place over h [rows][256].  Form nw:
 //   0 = choose; 3 / 4 = 96 / 128-row tiles of 32 x 256 wave blocks (3 / 4 waves);
 //   1 = 96-row tiles of 3 x 4 waves with 32 x 64 blocks (12 waves, all four SIMDs busy);
-//   2 = 64-row tiles of 2 x 4 waves.
-// One workgroup per CU (LDS).  Callers pad rows to 256; a tile never reads X past
-// round_up(rows, 256) (96-row tiles only when round_up(rows, 96) stays inside).
+//   2 = 64-row tiles of 2 x 4 waves; 8 = 128-row tiles of 4 x 4 waves.
+// One workgroup per CU (LDS).  Callers pad X and h to kWalkerRowPad (768 = lcm(96, 256))
+// rows, so no tile reads past them.
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat) {
   if (mode != 0) feat = X6Feat{};
-  const bool r96 = round_up(rows, 96) <= round_up(rows, 256);
-  if (nw < 1 || nw > 7 || (!r96 && (nw == 1 || nw == 3 || nw == 5 || nw == 6))) nw = r96 ? 1 : 2;
+  if (nw >= 32) {  // tools/ln_gemm_bench.py only: ablations / forced forms (caller pads rows to 768)
+    switch (nw) {
+#define DH_X6LN_A(TNV, NWV, WNV, ABLV)                                                                      \
+  launch_x6d_t<TNV, ABLV, NWV, 3, 2, WNV>(X, ldx, Wp, ldp, bias, h, 256, h, 256, rows, 256, K, 1, s, ln)
+      case 32: DH_X6LN_A(2, 2, 4, 1); break;
+      case 33: DH_X6LN_A(2, 2, 4, 2); break;
+      case 34: DH_X6LN_A(2, 2, 4, 3); break;
+      case 35: DH_X6LN_A(2, 2, 4, 4); break;
+      case 36: DH_X6LN_A(2, 3, 4, 0); break;
+      case 37: DH_X6LN_A(2, 3, 4, 4); break;
+      case 38: DH_X6LN_A(2, 4, 4, 0); break;
+      case 39: DH_X6LN_A(2, 4, 4, 4); break;
+      case 40: DH_X6LN_A(2, 2, 4, 5); break;
+      case 41: DH_X6LN_A(2, 3, 4, 5); break;
+      case 42: DH_X6LN_A(2, 3, 4, 6); break;
+      case 43: DH_X6LN_A(2, 3, 4, 7); break;
+#undef DH_X6LN_A
+    }
+    return;
+  }
+  if (nw == 0) {
+    // one workgroup per CU: the launch runs in rounds of cu_count tiles, so take the tile
+    // height with the least rounds x per-round time (MI355X, tools/ln_gemm_ablate.py:
+    // 64 / 96 / 128-row tiles ~23 / 28 / 30.5 us a round at K = 256; C2 24576 rows -> 96,
+    // C4 40960 -> 96, C5 81920 -> 128)
+    const int cus = cu_count_x6();
+    const int bm[3] = {96, 128, 64}, cost[3] = {280, 305, 230}, form[3] = {1, 8, 2};
+    long best = -1;
+    for (int q = 0; q < 3; ++q) {
+      const long t = (long)(((rows + bm[q] - 1) / bm[q] + cus - 1) / cus) * cost[q];
+      if (best < 0 || t < best) {
+        best = t;
+        nw = form[q];
+      }
+    }
+  }
+  if (nw < 1 || nw > 8) nw = 1;
 #define DH_X6LN_ST(TNV, NWV, WNV, STV)                                                                      \
   do {                                                                                                      \
     if (mode == 0)                                                                                          \
@@ -1668,6 +1772,7 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
     case 5: DH_X6LN_ST(2, 3, 4, 5); break;
     case 6: DH_X6LN_ST(2, 3, 4, 4); break;
     case 7: DH_X6LN_ST(2, 2, 4, 5); break;
+    case 8: DH_X6LN(2, 4, 4); break;
     default: DH_X6LN(8, 4, 1);
   }
 #undef DH_X6LN

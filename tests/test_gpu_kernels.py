@@ -164,8 +164,8 @@ def test_gemm_layernorm_fused(cuda, mode, bm, rows):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("nw", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("rows", [96, 1000, 24576])
+@pytest.mark.parametrize("nw", [0, 1, 2, 3, 4, 8])
+@pytest.mark.parametrize("rows", [96, 1000, 24576, 40960])
 def test_gemm_x6_layernorm_fused(cuda, mode, nw, rows):
     """Split-bf16 log-psi GEMM with the LayerNorm in its epilogue (in place over h): same
     contract and tolerance as the exact-f32 gemm_ln_kernel above, against float64."""
