@@ -78,6 +78,46 @@ __device__ __forceinline__ void split3(const float4& u, const float4& v, bf16x8&
   l = __builtin_bit_cast(bf16x8, Lv);
 }
 
+// One k-tile of split-bf16 products over TN column blocks with the B fragments of block
+// j + 1 read from LDS while block j's six MFMAs issue, and in the last block the NEXT
+// k-tile's block-0 fragments (from Bn: that stage has landed, the barrier at the top of
+// the k-tile saw to it), carried in nb.  sched_barrier keeps the reads ahead: left to
+// itself the compiler sinks each block's reads to just before its MFMAs and the first
+// MFMA of every block waits out the LDS latency.  The next k-tile's A split runs after
+// block TN / 2 (on zeros past the last k-tile).
+template <int TN, int B_PLANE>
+__device__ __forceinline__ void ktile_pipelined(const char* Bs, const char* Bn, f32x16 (&acc)[TN], bf16x8 (&nb)[3],
+                                                const bf16x8& c0, const bf16x8& c1, const bf16x8& c2,
+                                                const float4& u, const float4& v, bf16x8& n0, bf16x8& n1,
+                                                bf16x8& n2) {
+  bf16x8 fb[2][3];
+  auto ld = [&](const char* base, int j, bf16x8(&d)[3]) __attribute__((always_inline)) {
+    d[0] = *reinterpret_cast<const bf16x8*>(base + j * 1024);
+    d[1] = *reinterpret_cast<const bf16x8*>(base + B_PLANE + j * 1024);
+    d[2] = *reinterpret_cast<const bf16x8*>(base + 2 * B_PLANE + j * 1024);
+  };
+  fb[0][0] = nb[0];
+  fb[0][1] = nb[1];
+  fb[0][2] = nb[2];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if (j + 1 < TN)
+      ld(Bs, j + 1, fb[(j + 1) & 1]);
+    else
+      ld(Bn, 0, nb);
+    __builtin_amdgcn_sched_barrier(0);  // the reads stay ahead of this block's MFMAs
+    const bf16x8 b0 = fb[j & 1][0], b1 = fb[j & 1][1], b2 = fb[j & 1][2];
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
+    if (j == TN / 2) split3(u, v, n0, n1, n2);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // One wave = 32 rows x (32*TN) columns; NW waves stacked along rows (BM = 32*NW).
 template <int NW, int TN, bool HAS_R>
 __global__ __launch_bounds__(NW * 64) void gemm_x6_kernel(const float* __restrict__ X, int ldx,
@@ -718,6 +758,13 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
   }
   int bcur = 0;
   bf16x8 rb0 = c0, rb1 = c1, rb2 = c2;  // ABL 3 operands
+  constexpr bool PB = A_LDS && A_SPLIT;  // B reads pipelined one column block ahead
+  bf16x8 nb[3];
+  if constexpr (PB) {
+    nb[0] = *reinterpret_cast<const bf16x8*>(smem + boff);
+    nb[1] = *reinterpret_cast<const bf16x8*>(smem + boff + B_PLANE);
+    nb[2] = *reinterpret_cast<const bf16x8*>(smem + boff + 2 * B_PLANE);
+  }
   for (int kt = 0; kt < nk; ++kt) {
     if (A_DMA) {
       if (ST > 3 && kt + ST - 2 < nk)  // stages kt + 2 .. kt + ST - 2 issued: they may stay in flight
@@ -732,7 +779,11 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
     if (A_DMA && kt + ST - 1 < nk) stage(kt + ST - 1, bnl);
     const bool more = kt + 1 < nk;
     float4 u, v;
-    if (more) {
+    if (PB) {  // the next stage's A (stale past the last k-tile: split but never used)
+      const char* An = smem + bn1 * STAGE;
+      u = *reinterpret_cast<const float4*>(An + aoff0);
+      v = *reinterpret_cast<const float4*>(An + aoff1);
+    } else if (more) {
       if (A_LDS) {
         const char* An = smem + bn1 * STAGE;  // ABL 3, 4: no LDS reads
         u = *reinterpret_cast<const float4*>(An + aoff0);
@@ -745,6 +796,9 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
     const char* Bs = smem + bcur * STAGE + boff;
     bf16x8 n0, n1, n2;
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (PB) {
+      ktile_pipelined<TN, B_PLANE>(Bs, smem + bn1 * STAGE + boff, acc, nb, c0, c1, c2, u, v, n0, n1, n2);
+    } else {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bf16x8 b0, b1, b2;
@@ -772,6 +826,7 @@ __global__ __launch_bounds__(NW * WN * 64) __attribute__((amdgpu_waves_per_eu(NW
           n2 = n0;
         }
       }
+    }
     }
     __builtin_amdgcn_s_setprio(0);
     if (more) {
@@ -1054,7 +1109,7 @@ void launch_x6d_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
 // doubles).  No LDS is left for a transpose region, so a tile's last step does not issue
 // its step + 3 DMA: the epilogue transposes through that free stage buffer, and the next
 // step issues two stages (its wait then counts the epilogue's stores instead).
-template <int TN, bool HAS_R, bool R4 = false, int ABLQ = 0>  // ABLQ 1: no epilogue stores (tools only)
+template <int TN, bool HAS_R, bool R4 = false, int ABLQ = 0, bool PB = false>  // ABLQ 1: no epilogue stores (tools only)
 __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__ X, int ldx,
                                                        const uint16_t* __restrict__ Wp, int ldp,
                                                        const float* __restrict__ bias, const float* R, int ldr,
@@ -1151,6 +1206,12 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
     const float4 v = *reinterpret_cast<const float4*>(smem + aoff1);
     split3(u, v, c0, c1, c2);
   }
+  bf16x8 nb[3];  // PB: block-0 B fragments of the current k-tile
+  if constexpr (PB) {
+    nb[0] = *reinterpret_cast<const bf16x8*>(smem + boff);
+    nb[1] = *reinterpret_cast<const bf16x8*>(smem + boff + B_PLANE);
+    nb[2] = *reinterpret_cast<const bf16x8*>(smem + boff + 2 * B_PLANE);
+  }
   int bcur = 0, kt = 0, tile = 0;
   bool stored = false;  // epilogue stores issued in the previous step
   bool deferred = false;  // R4: the previous (tile-end) step left its step + 3 DMA to this one
@@ -1191,7 +1252,11 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
     }
     const bool more = f + 1 < F;
     float4 u, v;
-    if (more) {
+    if (PB) {  // the next stage's A (stale past the last k-tile: split but never used)
+      const char* An = smem + bn1 * STAGE;
+      u = *reinterpret_cast<const float4*>(An + aoff0);
+      v = *reinterpret_cast<const float4*>(An + aoff1);
+    } else if (more) {
       const char* An = smem + bn1 * STAGE;
       u = *reinterpret_cast<const float4*>(An + aoff0);
       v = *reinterpret_cast<const float4*>(An + aoff1);
@@ -1199,6 +1264,9 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
     const char* Bs = smem + bcur * STAGE + boff;
     bf16x8 n0, n1, n2;
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (PB) {
+      ktile_pipelined<TN, B_PLANE>(Bs, smem + bn1 * STAGE + boff, acc, nb, c0, c1, c2, u, v, n0, n1, n2);
+    } else {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bs + j * 1024);
@@ -1211,6 +1279,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
       if (j == TN / 2 && more) split3(u, v, n0, n1, n2);
+    }
     }
     __builtin_amdgcn_s_setprio(0);
     if (more) {
@@ -1321,7 +1390,7 @@ __global__ __launch_bounds__(512) void gemm_x6q_kernel(const float* __restrict__
   }
 }
 
-template <int TN, bool R4 = false, int ABLQ = 0>
+template <int TN, bool R4 = false, int ABLQ = 0, bool PB = false>
 void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* R, int ldr,
                   float* Y, int ldy, int rows, int ncols, int K, int C, hipStream_t s) {
   constexpr int BM = 256, BN = 32 * TN;
@@ -1332,12 +1401,12 @@ void launch_x6q_t(const float* X, int ldx, const uint16_t* Wp, int ldp, const fl
   int grid = std::min(ntm * ntn, cu_count_x6());
   grid = std::max(8, grid / 8 * 8);
   if (R) {
-    ensure_smem(gemm_x6q_kernel<TN, true, R4, ABLQ>, smem);
-    hipLaunchKernelGGL((gemm_x6q_kernel<TN, true, R4, ABLQ>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R,
+    ensure_smem(gemm_x6q_kernel<TN, true, R4, ABLQ, PB>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, true, R4, ABLQ, PB>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias, R,
                        ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
   } else {
-    ensure_smem(gemm_x6q_kernel<TN, false, R4, ABLQ>, smem);
-    hipLaunchKernelGGL((gemm_x6q_kernel<TN, false, R4, ABLQ>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias,
+    ensure_smem(gemm_x6q_kernel<TN, false, R4, ABLQ, PB>, smem);
+    hipLaunchKernelGGL((gemm_x6q_kernel<TN, false, R4, ABLQ, PB>), dim3(grid), dim3(512), smem, s, X, ldx, Wp, ldp, bias,
                        R, ldr, Y, ldy, rows, ncols, K, C, ntm, ntn);
   }
 }
@@ -1652,6 +1721,16 @@ void launch_gemm_x6_variant(int v, const float* X, int ldx, const uint16_t* Wp, 
     case 55:
       launch_x6q_t<5>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
+    // persistent lean with the B fragment reads pipelined one column block ahead
+    case 56:
+      launch_x6q_t<8, false, 0, true>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 57:
+      launch_x6q_t<6, false, 0, true>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
+    case 58:
+      launch_x6q_t<5, false, 0, true>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
+      break;
     case 95:  // ablation of 50: no epilogue stores (wrong results; tools/gemm_bench.py only)
       launch_x6q_t<8, false, 1>(X, ldx, Wp, ldp, bias, R, ldr, Y, ldy, rows, ncols, K, C, s);
       break;
@@ -1683,12 +1762,13 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
   // were no faster at these shapes (tools/ln_gemm_bench.py).
   // Channel rows: below 1024 columns the width with the least padding (C4's orbital map,
   // 480 columns: 256-wide 2125 us, 192-wide 1816 us, 160-wide 1628 us; tools/gemm_orb_bench.py),
-  // else 256 (C5's 2320 columns: 12.9 ms against 13.8 ms 160-wide)
+  // else 256 (C5's 2320 columns: 12.9 ms against 13.8 ms 160-wide); the B fragment reads
+  // pipelined one column block ahead (56-58: el_qkv 968 -> 932 us, tools/gemm_bench.py)
   int v;
   if (rows >= 65536) {
-    v = 50;
+    v = 56;
     if (ncols < 1024) {
-      const int tns[4] = {8, 6, 5, 4}, vs[4] = {50, 51, 55, 52};
+      const int tns[4] = {8, 6, 5, 4}, vs[4] = {56, 57, 58, 52};
       int best = round_up(ncols, 256);
       for (int q = 1; q < 4; ++q) {
         const int padded = round_up(ncols, 32 * tns[q]);
