@@ -612,6 +612,9 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // log psi, split-bf16: layer 1's residual h = features W0 is formed in the epilogue of
   // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
   const bool h_feat = C == 1 && fused && x6 && ln_fused;
+  // log psi, split-bf16, D = 256: each layer's tail (Wo Wl + LN1, Wm + LN2) and the next
+  // linear map (the next layer's q|k|v, or the orbitals) run as ONE launch (chain_x6_kernel)
+  const bool chain = C == 1 && x6 && ln_fused && D == 256 && chain_x6_enabled();
   {
     const bool wq = fold && !fused;
     PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
@@ -620,11 +623,21 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0) gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    if (l > 0 && !chain) gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
+    }
+    if (chain) {
+      const bool last = l + 1 == d.L;
+      const int n3 = last ? d.orb_cols : 3 * D;
+      PROF(PK_GEMM, 2.0 * R * DD * (2.0 * DD + n3), f4 * (2.0 * R * DD + R * n3 + 2.0 * DD * DD + DD * n3));
+      launch_chain_x6(w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
+                      last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
+                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows,
+                      (h_feat && l == 0) ? X6Feat{P.W0, w.geo, d.N, d.n_up} : X6Feat{}, s);
+      continue;
     }
     if (ln_fused) {
       // log psi: each GEMM carries its LayerNorm in the epilogue, in place over h
@@ -657,7 +670,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
+  if (!chain || d.L == 0)
+    gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
 
@@ -1069,6 +1083,17 @@ int dh_debug_gemm_x6_ln(int mode, int nw, const float* X, int ldx, const uint16_
   if (!gemm_x6_supported(K) || K > 256 || ldp < x6_plane_rows(256) || rows < 1 || (mode != 0 && mode != 1))
     return fail(DH_EINVAL, "bad gemm_x6_ln args");
   launch_gemm_x6_ln(X, ldx, Wp, ldp, bias, ln, h, rows, K, mode, nw, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_debug_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3,
+                      int ldp3, const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, void* stream) {
+  if (!X1 || !Wp1 || !Wp2 || !b1 || !ln1 || !b2 || !ln2 || !h || rows < 1 || ldp1 < x6_plane_rows(256) ||
+      ldp2 < x6_plane_rows(256) || (Wp3 && (!b3 || !Y3 || n3 < 1 || ldy3 < n3 || ldy3 % 4 || ldp3 < x6_plane_rows(n3))))
+    return fail(DH_EINVAL, "bad chain_x6 args");
+  launch_chain_x6(X1, Wp1, ldp1, b1, ln1, Wp2, ldp2, b2, ln2, Wp3, ldp3, b3, n3, Y3, ldy3, h, rows, X6Feat{},
+                  (hipStream_t)stream);
   return check_launch();
 }
 

@@ -110,6 +110,12 @@ struct X6Feat {
 };
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
+bool chain_x6_enabled();
+// Log-psi layer tail in one launch (D = K = 256): h1 = LN1(h + X1 Wol + b1) (feature
+// residual when feat.W0), h = LN2(h1 + tanh(h1 Wm + b2)), then Y3 = h W3 + b3 if Wp3.
+void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s);
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).
 void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s);
 

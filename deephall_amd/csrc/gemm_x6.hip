@@ -25,6 +25,8 @@
 // the tile and all BN = 32*TN columns, so every activation element is split exactly
 // once.  B planes are staged by LDS-DMA into [plane][BN][64 B] images, 16-B slots
 // swizzled by (row>>2)&3 (16 lanes of a ds_read_b128 pass hit 16 distinct bank groups).
+#include <cstdlib>
+
 #include "dh_internal.h"
 #include "device_common.h"
 
@@ -1570,6 +1572,285 @@ __global__ void split_planes_kernel(const float* __restrict__ Wt, int ldw, int n
   Wp[2 * plane + i] = __builtin_bit_cast(uint16_t, a2);
 }
 
+
+// ---- chained log-psi layer tail ------------------------------------------------------------
+// One launch per layer for the walker rows (C = 1) of the split-bf16 log-psi path:
+//   P1  h1 = LN1(h + o Wol + bol)                (psiformer.py:44-46; Wol = Wo Wl folded)
+//   P2  h2 = LN2(h1 + tanh(h1 Wm + bm))           (psiformer.py:47-48)  -> h (global)
+//   P3  Y3 = h2 W3 + b3   (optional)              the next layer's q|k|v, or the orbitals
+// A 96-row tile (16 walkers at N = 6) of 3 x 4 waves (32 x 64 wave blocks, as the 96-row
+// LayerNorm GEMM) keeps h1 and h2 in LDS: P2 and P3 take their A operand from that tile
+// (no HBM round trip of h1, no re-read of h2, two launches fewer); only the B planes stream
+// through a two-stage LDS-DMA ring.  LDS: tile 96 x 260 f32 (99 840 B) + ring 2 x 30 720 B.
+// The arithmetic (k order, splits, LayerNorm statistics, tanh) is that of the separate
+// kernels, so the results are bitwise the same (tests/test_gpu_kernels.py).
+constexpr int CH_NW = 3, CH_WN = 4, CH_NWT = 12, CH_TN = 2, CH_BM = 96, CH_BN = 256, CH_LS = 260, CH_K = 256;
+constexpr int CH_A = CH_BM * 16 * 4, CH_BP = CH_BN * 16 * 2, CH_STAGE = CH_A + 3 * CH_BP;
+constexpr size_t CH_TILE = (size_t)CH_BM * CH_LS * 4, CH_SMEM = CH_TILE + 2 * CH_STAGE;
+static_assert(CH_SMEM <= 163840, "chain LDS");
+
+struct ChainArgs {
+  const float* X1;  // o [rows][256]
+  const uint16_t *Wp1, *Wp2, *Wp3;
+  int ldp1, ldp2, ldp3;
+  const float *b1, *ln1, *b2, *ln2, *b3;
+  int n3, ldy3;
+  float* Y3;
+  float* h;  // residual of P1 (unless feat.W0), output of P2
+  int rows;
+  X6Feat feat;
+};
+
+__global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
+  constexpr int TN = CH_TN, NWT = CH_NWT, LS = CH_LS, nk = CH_K / 16;
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  float* tile = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / CH_WN, wn = wid % CH_WN;
+  const int l32 = lane & 31, lh = lane >> 5;
+  int bid = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int row0 = bid * CH_BM, rows = a.rows;
+  const uint32_t ring0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)(smem + CH_TILE));
+  const int m = wm * 32 + l32;
+  // A fragments: ring image (phase 1, swizzled as x6d) or the f32 tile (phases 2, 3)
+  const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
+  const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
+  const int boff = CH_A + wn * TN * 1024 + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
+
+  // DMA of k-tile kt into ring buffer buf: (A pieces 0..5 when xa) + 24 B pieces (1 KB each)
+  auto stage = [&](const char* xa, const char* wb, int ldp, int kt, int buf) __attribute__((always_inline)) {
+    const int IA = xa ? CH_A / 1024 : 0, tot = IA + (3 * CH_BP) / 1024;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int j = wid + t * NWT;
+      if (j >= tot) break;  // wave-uniform
+      uint32_t voff, ldst;
+      const char* base;
+      if (j < IA) {  // 16 rows x 64 B of f32 activations
+        const int r = j * 16 + (lane >> 2);
+        const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
+        voff = (uint32_t)(r * CH_K + sl) * 4u;
+        ldst = j * 1024;
+        base = xa + kt * 64;
+      } else {  // 32 rows x 32 B of the weight planes
+        const int q = (j - IA) * 32 + (lane >> 1);
+        const int p = q / CH_BN, n = q % CH_BN;
+        const int sl = ((lane & 1) ^ ((n >> 3) & 1)) * 8;
+        voff = (uint32_t)(((size_t)p * ldp + n) * CH_K + sl) * 2u;
+        ldst = CH_A + (j - IA) * 1024;
+        base = wb + kt * 32;
+      }
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + (uint32_t)(buf * CH_STAGE) + ldst);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(voff), "s"(base), "s"(dst)
+                   : "memory");
+    }
+  };
+  // one GEMM pass over K = 256 (two-buffer ring: k-tile kt+1 lands while kt computes)
+  f32x16 acc[TN];
+  auto gemm = [&](const char* xa, const char* wb, int ldp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    stage(xa, wb, ldp, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(xa, wb, ldp, kt + 1, cur ^ 1);
+      float4 u, v;
+      if (xa) {
+        const char* As = smem + CH_TILE + cur * CH_STAGE;
+        u = *reinterpret_cast<const float4*>(As + aoff0);
+        v = *reinterpret_cast<const float4*>(As + aoff1);
+      } else {
+        const float* tr = tile + m * LS + 16 * kt + 8 * lh;
+        u = *reinterpret_cast<const float4*>(tr);
+        v = *reinterpret_cast<const float4*>(tr + 4);
+      }
+      bf16x8 c0, c1, c2;
+      split3(u, v, c0, c1, c2);
+      const char* Bc = smem + CH_TILE + cur * CH_STAGE + boff;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bc + j * 1024);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bc + CH_BP + j * 1024);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bc + 2 * CH_BP + j * 1024);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k-tile kt+1 landed
+      __syncthreads();                                  // ... and buffer cur is free
+    }
+  };
+  // acc (MFMA layout: reg e of acc[j] = row m, column 32 (wn TN + j) + 8 (e >> 2) + 4 lh + (e & 3))
+  auto acc_pos = [&](int j, int g) __attribute__((always_inline)) { return m * LS + 32 * (wn * TN + j) + 8 * g + 4 * lh; };
+  auto acc_col = [&](int j, int g) __attribute__((always_inline)) { return 32 * (wn * TN + j) + 8 * g + 4 * lh; };
+  // row LayerNorm of the tile in place: 16 lanes per row, 4 rows per pass (as the LNM
+  // epilogue of gemm_x6d_kernel); optional residual (R rows or feature residual) and bias
+  // added first; optional copy of the result to global rows of Yg
+  const int sub = lane & 15, rq = lane >> 4;
+  constexpr int NP = CH_BM / (4 * NWT);  // 2 passes
+  auto ln_rows = [&](const float* bias, const float* ln, const float* R, bool feat, float* Yg) __attribute__((always_inline)) {
+    float4 rpre[NP][4];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int r = row0 + 4 * (wid + NWT * p) + rq;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        rpre[p][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < rows) {
+          if (feat) {
+            if (k == 0) rpre[p][0] = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);
+          } else if (R) {
+            rpre[p][k] = *reinterpret_cast<const float4*>(R + (size_t)r * CH_BN + 4 * sub + 64 * k);
+          }
+        }
+      }
+    }
+    float4 bv[4], gm[4], bt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * sub + 64 * k;
+      bv[k] = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      gm[k] = *reinterpret_cast<const float4*>(ln + c);
+      bt[k] = *reinterpret_cast<const float4*>(ln + CH_BN + c);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int rr = 4 * (wid + NWT * p) + rq;
+      const int r = row0 + rr;
+      float f[4];
+      if (feat) {
+        const float4 g = rpre[p][0];  // st ct sp cp
+        f[0] = g.y;
+        f[1] = g.x * g.w;
+        f[2] = g.x * g.z;
+        f[3] = (r % a.feat.N < a.feat.n_up) ? 1.f : -1.f;
+      }
+      float4 v[4];
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * sub + 64 * k;
+        float4 t = *reinterpret_cast<const float4*>(tile + rr * LS + c);
+        t.x += bv[k].x;
+        t.y += bv[k].y;
+        t.z += bv[k].z;
+        t.w += bv[k].w;
+        if (r < rows && (feat || R)) {
+          float4 rv;
+          if (feat) {
+            float4 w0[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w0[q] = *reinterpret_cast<const float4*>(a.feat.W0 + q * CH_BN + c);
+            rv.x = f[0] * w0[0].x + f[1] * w0[1].x + f[2] * w0[2].x + f[3] * w0[3].x;
+            rv.y = f[0] * w0[0].y + f[1] * w0[1].y + f[2] * w0[2].y + f[3] * w0[3].y;
+            rv.z = f[0] * w0[0].z + f[1] * w0[1].z + f[2] * w0[2].z + f[3] * w0[3].z;
+            rv.w = f[0] * w0[0].w + f[1] * w0[1].w + f[2] * w0[2].w + f[3] * w0[3].w;
+          } else {
+            rv = rpre[p][k];
+          }
+          t.x += rv.x;
+          t.y += rv.y;
+          t.z += rv.z;
+          t.w += rv.w;
+        }
+        v[k] = t;
+        sum += (t.x + t.y) + (t.z + t.w);
+      }
+      const float mean = row16_sum(sum) * (1.f / 256.f);
+      float ss = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k].x -= mean;
+        v[k].y -= mean;
+        v[k].z -= mean;
+        v[k].w -= mean;
+        ss += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
+      }
+      const float var = row16_sum(ss) * (1.f / 256.f);
+      const float rs = __builtin_amdgcn_rsqf(var + 1e-5f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float4 o;
+        o.x = gm[k].x * (rs * v[k].x) + bt[k].x;
+        o.y = gm[k].y * (rs * v[k].y) + bt[k].y;
+        o.z = gm[k].z * (rs * v[k].z) + bt[k].z;
+        o.w = gm[k].w * (rs * v[k].w) + bt[k].w;
+        *reinterpret_cast<float4*>(tile + rr * LS + 4 * sub + 64 * k) = o;
+        if (Yg && r < rows) *reinterpret_cast<float4*>(Yg + (size_t)r * CH_BN + 4 * sub + 64 * k) = o;
+      }
+    }
+  };
+
+  // ---- P1: h1 = LN1(h + o Wol + bol) into the tile
+  gemm(reinterpret_cast<const char*>(a.X1 + (size_t)row0 * CH_K), reinterpret_cast<const char*>(a.Wp1), a.ldp1);
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(tile + acc_pos(j, g)) =
+          make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
+  __syncthreads();
+  ln_rows(a.b1, a.ln1, a.feat.W0 ? nullptr : a.h, a.feat.W0 != nullptr, nullptr);
+  __syncthreads();
+  // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) into the tile and h
+  gemm(nullptr, reinterpret_cast<const char*>(a.Wp2), a.ldp2);  // ends with a barrier: the tile is free
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4* tp = reinterpret_cast<float4*>(tile + acc_pos(j, g));
+      const float4 bv = *reinterpret_cast<const float4*>(a.b2 + acc_col(j, g));
+      const float4 r = *tp;
+      *tp = make_float4(r.x + tanh_rat(acc[j][4 * g] + bv.x), r.y + tanh_rat(acc[j][4 * g + 1] + bv.y),
+                        r.z + tanh_rat(acc[j][4 * g + 2] + bv.z), r.w + tanh_rat(acc[j][4 * g + 3] + bv.w));
+    }
+  __syncthreads();
+  ln_rows(nullptr, a.ln2, nullptr, false, a.h);
+  if (!a.Wp3) return;
+  __syncthreads();
+  // ---- P3: Y3 = h2 W3 + b3, 256-column tiles, stored from the MFMA layout (16-B pieces)
+  for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
+    gemm(nullptr, reinterpret_cast<const char*>(a.Wp3 + (size_t)col0 * CH_K), a.ldp3);
+    const int r = row0 + m;
+    if (r < rows) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = col0 + acc_col(j, g);
+          float* yr = a.Y3 + (size_t)r * a.ldy3;
+          if (c + 3 < a.n3) {
+            const float4 bv = *reinterpret_cast<const float4*>(a.b3 + c);
+            *reinterpret_cast<float4*>(yr + c) = make_float4(acc[j][4 * g] + bv.x, acc[j][4 * g + 1] + bv.y,
+                                                             acc[j][4 * g + 2] + bv.z, acc[j][4 * g + 3] + bv.w);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c + e < a.n3) yr[c + e] = acc[j][4 * g + e] + a.b3[c + e];
+          }
+        }
+    }
+  }
+}
+
 }  // namespace
 
 int x6_plane_rows(int ncols) { return round_up(ncols, kRowPad) + kRowPad; }
@@ -1857,6 +2138,25 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
   }
 #undef DH_X6LN
 #undef DH_X6LN_ST
+}
+
+// DH_CHAIN=0 keeps the separate LayerNorm GEMMs (A/B measurements)
+bool chain_x6_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_CHAIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Chained log-psi layer tail (chain_x6_kernel above).  X1 and h padded to kWalkerRowPad
+// rows; Wp3 may be null (no P3); Y3 rows 16-B aligned (ldy3 % 4 == 0).
+void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s) {
+  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, feat};
+  ensure_smem(chain_x6_kernel, CH_SMEM);
+  hipLaunchKernelGGL(chain_x6_kernel, dim3((rows + CH_BM - 1) / CH_BM), dim3(768), CH_SMEM, s, a);
 }
 
 }  // namespace dh

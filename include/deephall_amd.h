@@ -278,6 +278,11 @@ int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt,
  * 2 = 64 rows x (2 x 4 waves), 3 / 4 = 96 / 128 rows of whole-row waves, 0 = choose. */
 int dh_debug_gemm_x6_ln(int mode, int nw, const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias,
                         const float* ln, float* h, int rows, int K, void* stream);
+/* Chained log-psi layer tail (gemm_x6.hip chain_x6_kernel; D = K = 256, rows padded to 768):
+ * h1 = LN1(h + X1 W1 + b1); h = LN2(h1 + tanh(h1 W2 + b2)); Y3 = h W3 + b3 when Wp3. */
+int dh_debug_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3,
+                      int ldp3, const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, void* stream);
 
 /* Test hooks of the split-bf16 GEMM (gemm_x6.hip): the transposed weight Wt[ncols][K]
  * is split into three bf16 planes Wp[3][ldp][K] (ldp = dh_debug_x6_plane_rows(ncols),

@@ -193,3 +193,59 @@ def test_gemm_x6_layernorm_fused(cuda, mode, nw, rows):
     err = (h[:rows].double() - ref).abs().max().item()
     assert err < 2e-4, err
     assert torch.equal(h[rows:], h0[rows:])
+
+
+@pytest.mark.parametrize("n3", [0, 768, 192, 18])
+@pytest.mark.parametrize("rows", [96, 1000, 24576, 40960])
+def test_chain_x6_matches_separate_kernels(cuda, n3, rows):
+    """The chained log-psi layer tail (one launch: LN1 GEMM, LN2 GEMM, next linear map) is
+    bitwise the separate split-bf16 kernels (same k order, splits, LayerNorm statistics),
+    and within f32 of the float64 layer."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(rows + n3)
+    K = D = 256
+    rp = (rows + 767) // 768 * 768
+    X1 = torch.randn(rp, K, generator=g).cuda()
+    h0 = torch.randn(rp, D, generator=g).cuda()
+    W1, W2 = ((torch.randn(K, D, generator=g) / 16).cuda() for _ in range(2))
+    b1, b2 = (torch.randn(D, generator=g).cuda() for _ in range(2))
+    ln1, ln2 = (torch.cat([1.0 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)]).cuda()
+                for _ in range(2))
+    Wp1, ldp = _x6_planes(lib, W1, D, K)
+    Wp2, _ = _x6_planes(lib, W2, D, K)
+    ldy = (n3 + 3) // 4 * 4 if n3 else 4
+    if n3:
+        W3 = (torch.randn(K, n3, generator=g) / 16).cuda()
+        b3 = torch.randn(n3, generator=g).cuda()
+        Wp3, ldp3 = _x6_planes(lib, W3, n3, K)
+    else:
+        W3 = b3 = Wp3 = None
+        ldp3 = 0
+    # separate kernels
+    h_sep = h0.clone()
+    assert lib.dh_debug_gemm_x6_ln(0, 0, _p(X1), K, _p(Wp1), ldp, _p(b1), _p(ln1), _p(h_sep), rows, K, _stream()) == 0
+    assert lib.dh_debug_gemm_x6_ln(1, 0, _p(h_sep), K, _p(Wp2), ldp, _p(b2), _p(ln2), _p(h_sep), rows, K, _stream()) == 0
+    Y_sep = torch.zeros(rp, ldy, device="cuda")
+    if n3:
+        assert lib.dh_debug_gemm_x6(-1, _p(h_sep), K, _p(Wp3), ldp3, _p(b3), None, 0, _p(Y_sep), ldy, rows, n3, K, 1,
+                                    _stream()) == 0
+    # chain
+    h_ch = h0.clone()
+    Y_ch = torch.zeros(rp, ldy, device="cuda")
+    assert lib.dh_debug_chain_x6(_p(X1), _p(Wp1), ldp, _p(b1), _p(ln1), _p(Wp2), ldp, _p(b2), _p(ln2), _p(Wp3), ldp3,
+                                 _p(b3), n3, _p(Y_ch), ldy, _p(h_ch), rows, _stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(h_ch[:rows], h_sep[:rows])
+    assert torch.equal(h_ch[rows:], h0[rows:])  # padding rows untouched
+    if n3:
+        assert torch.equal(Y_ch[:rows, :n3], Y_sep[:rows, :n3])
+    # float64 layer
+    def ln(y, p):
+        mu = y.mean(-1, keepdim=True)
+        return (y - mu) / torch.sqrt(((y - mu) ** 2).mean(-1, keepdim=True) + 1e-5) * p[:D].double() + p[D:].double()
+    h1 = ln(h0[:rows].double() + X1[:rows].double() @ W1.double() + b1.double(), ln1)
+    h2 = ln(h1 + torch.tanh(h1 @ W2.double() + b2.double()), ln2)
+    assert (h_ch[:rows].double() - h2).abs().max().item() < 2e-4
+    if n3:
+        y = h2 @ W3.double() + b3.double()
+        assert (Y_ch[:rows, :n3].double() - y).abs().max().item() < 2e-4 * max(1.0, y.abs().max().item())
