@@ -1851,6 +1851,305 @@ __global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
   }
 }
 
+
+// ---- chained layer tail, pre-split activations ------------------------------------------------
+// The production form.  As chain_x6_kernel, but every activation element is split into its
+// three bf16 terms ONCE, by the thread that writes it, into LDS planes [3][96][264] (the
+// x6d/x6r forms re-split the A tile in every wave that reads it: 4-8x the VALU work, the
+// largest cost left in the pass, tools/chain_bench.py), and the weight fragments stream
+// from L2 straight into registers PD k-tiles ahead (no LDS ring, no barrier in a pass).
+// 8 waves; wave w owns output columns 32 w .. 32 w + 31 of a 256-column pass and all 96
+// rows (three 32-row MFMA blocks).  The LayerNorms run on the MFMA layout in registers:
+// row sums = 16 values per lane + the lane-half shuffle + 8 wave partials through LDS.
+// Same products in the same order as the other x6 kernels; the LayerNorm statistics are
+// summed in a different order (f32 rounding, not bitwise).
+constexpr int CS_NW = 8, CS_RB = CH_BM / 32, CS_PD = 4, CS_LSP = 264;  // plane row: 528 B
+constexpr size_t CS_PLANE = (size_t)CH_BM * CS_LSP * 2, CS_SMEM = 3 * CS_PLANE + 2 * CS_NW * CH_BM * 4;
+static_assert(CS_SMEM <= 163840, "chain LDS");
+
+// 4 f32 -> three packed bf16 pairs per term (as split3)
+__device__ __forceinline__ void split4(const float4& x, uint2& h, uint2& m, uint2& l) {
+  const float a[4] = {x.x, x.y, x.z, x.w};
+  uint32_t H[2], Mv[2], Lv[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float u = a[2 * p], v = a[2 * p + 1];
+    const uint32_t h2 = pk_bf16(u, v);
+    const float ru = u - lo_f(h2), rv = v - hi_f(h2);
+    const uint32_t m2 = pk_bf16(ru, rv);
+    H[p] = h2;
+    Mv[p] = m2;
+    Lv[p] = pk_bf16(ru - lo_f(m2), rv - hi_f(m2));
+  }
+  h = make_uint2(H[0], H[1]);
+  m = make_uint2(Mv[0], Mv[1]);
+  l = make_uint2(Lv[0], Lv[1]);
+}
+
+template <int ABLS = 0>  // ABLS (tools only): 1 weight fragments from one k-tile (L1-resident); 2 no P3 stores
+__global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
+  constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  int bid = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int row0 = bid * CH_BM, rows = a.rows;
+  // plane p, tile row r, column c (bf16 units)
+  auto pl = [&](int p, int r, int c) __attribute__((always_inline)) {
+    return smem + (size_t)p * CS_PLANE + (size_t)r * (LSP * 2) + c * 2;
+  };
+  // write 4 consecutive f32 of row r, columns c..c+3 as their three bf16 terms
+  auto put4 = [&](int r, int c, const float4& x) __attribute__((always_inline)) {
+    uint2 h, m, l;
+    split4(x, h, m, l);
+    *reinterpret_cast<uint2*>(pl(0, r, c)) = h;
+    *reinterpret_cast<uint2*>(pl(1, r, c)) = m;
+    *reinterpret_cast<uint2*>(pl(2, r, c)) = l;
+  };
+  // the f32 value back from the planes (exact: a = a0 + a1 + a2 with no rounding)
+  auto get4 = [&](int r, int c) __attribute__((always_inline)) {
+    const uint2 h = *reinterpret_cast<const uint2*>(pl(0, r, c));
+    const uint2 m = *reinterpret_cast<const uint2*>(pl(1, r, c));
+    const uint2 l = *reinterpret_cast<const uint2*>(pl(2, r, c));
+    return make_float4((lo_f(h.x) + lo_f(m.x)) + lo_f(l.x), (hi_f(h.x) + hi_f(m.x)) + hi_f(l.x),
+                       (lo_f(h.y) + lo_f(m.y)) + lo_f(l.y), (hi_f(h.y) + hi_f(m.y)) + hi_f(l.y));
+  };
+
+  // ---- one GEMM pass: acc[rb] = rows 32 rb + l32 x columns col0 + 32 wid + ..  The weight
+  // fragments of its first PD k-tiles are requested by prefetch() beforehand, ahead of the
+  // previous pass's epilogue: its stores then do not sit in front of them in vmcnt's queue
+  f32x16 acc[RB];
+  bf16x8 bq[PD][3];
+  const uint16_t* wr = nullptr;
+  size_t plane = 0;
+  auto prefetch = [&](const uint16_t* Wp, int ldp, int col0) __attribute__((always_inline)) {
+    plane = (size_t)ldp * CH_K;
+    wr = Wp + (size_t)(col0 + 32 * wid + l32) * CH_K + 8 * lh;
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
+  };
+  auto gemm = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[rb][e] = 0.f;
+    // A fragments of k-tile kt (rows 32 rb + l32, k = 16 kt + 8 lh ..), read one k-tile ahead
+    bf16x8 ca[RB][3];
+    auto lda = [&](int kt, bf16x8(&d)[RB][3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          d[rb][p] = *reinterpret_cast<const bf16x8*>(pl(p, 32 * rb + l32, 16 * kt + 8 * lh));
+    };
+    lda(0, ca);
+#pragma unroll
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16x8 b0 = bq[kt % PD][0], b1 = bq[kt % PD][1], b2 = bq[kt % PD][2];
+      if (kt + PD < nk) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bq[kt % PD][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + (ABLS ? 0 : 16 * (kt + PD)));
+      }
+      bf16x8 cn[RB][3];
+      if (kt + 1 < nk) lda(kt + 1, cn);
+      // keep the prefetches where they are: the scheduler would sink each load to just
+      // before its first use and expose the L2 / LDS latency
+      __builtin_amdgcn_sched_barrier(0);
+      // product-major over the three row blocks: consecutive MFMAs are independent
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][2], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, ca[rb][0], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][1], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][1], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][0], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][0], acc[rb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) ca[rb][p] = cn[rb][p];
+      }
+    }
+  };
+  // MFMA layout: reg 4 g + e of acc[rb] = tile row 32 rb + l32, column 32 wid + 8 g + 4 lh + e
+  auto colof = [&](int g) __attribute__((always_inline)) { return 32 * wid + 8 * g + 4 * lh; };
+  // LayerNorm of the values x (MFMA layout, 16 per lane and row block) in registers:
+  // two-pass mean / centred variance (eps 1e-5); the 8 wave partials of a row meet in LDS
+  float x[RB][16];
+  auto layernorm = [&](const float* ln) __attribute__((always_inline)) {
+    float s[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) t += (x[rb][4 * g] + x[rb][4 * g + 1]) + (x[rb][4 * g + 2] + x[rb][4 * g + 3]);
+      t += __shfl_xor(t, 32, 64);
+      if (lh == 0) part[wid * CH_BM + 32 * rb + l32] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < CS_NW; ++w) t += part[w * CH_BM + 32 * rb + l32];
+      s[rb] = t * (1.f / 256.f);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        x[rb][e] -= s[rb];
+        q += x[rb][e] * x[rb][e];
+      }
+      q += __shfl_xor(q, 32, 64);
+      if (lh == 0) part[(CS_NW + wid) * CH_BM + 32 * rb + l32] = q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < CS_NW; ++w) t += part[(CS_NW + w) * CH_BM + 32 * rb + l32];
+      const float rs = __builtin_amdgcn_rsqf(t * (1.f / 256.f) + 1e-5f);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gm = *reinterpret_cast<const float4*>(ln + colof(g));
+        const float4 bt = *reinterpret_cast<const float4*>(ln + CH_BN + colof(g));
+        x[rb][4 * g] = gm.x * (rs * x[rb][4 * g]) + bt.x;
+        x[rb][4 * g + 1] = gm.y * (rs * x[rb][4 * g + 1]) + bt.y;
+        x[rb][4 * g + 2] = gm.z * (rs * x[rb][4 * g + 2]) + bt.z;
+        x[rb][4 * g + 3] = gm.w * (rs * x[rb][4 * g + 3]) + bt.w;
+      }
+    }
+  };
+
+  // ---- P1 prologue: o rows -> planes (each element split once)
+  prefetch(a.Wp1, a.ldp1, 0);
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
+#pragma unroll 4
+    for (int i = tid; i < CH_BM * (CH_K / 4); i += 512) {
+      const int r = i / (CH_K / 4), c = 4 * (i % (CH_K / 4));
+      put4(r, c, src[i]);
+    }
+    __syncthreads();
+  }
+  // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
+  gemm();
+  prefetch(a.Wp2, a.ldp2, 0);
+  {
+    float4 w0[4][4];  // feature residual: W0 rows at this lane's columns
+    if (a.feat.W0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w0[g][q] = *reinterpret_cast<const float4*>(a.feat.W0 + q * CH_BN + colof(g));
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = row0 + 32 * rb + l32;
+      float f[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.feat.W0) {
+        const float4 gq = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
+        f[0] = gq.y;
+        f[1] = gq.x * gq.w;
+        f[2] = gq.x * gq.z;
+        f[3] = (r % a.feat.N < a.feat.n_up) ? 1.f : -1.f;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 bv = *reinterpret_cast<const float4*>(a.b1 + colof(g));
+        float4 rv;
+        if (a.feat.W0) {
+          rv.x = f[0] * w0[g][0].x + f[1] * w0[g][1].x + f[2] * w0[g][2].x + f[3] * w0[g][3].x;
+          rv.y = f[0] * w0[g][0].y + f[1] * w0[g][1].y + f[2] * w0[g][2].y + f[3] * w0[g][3].y;
+          rv.z = f[0] * w0[g][0].z + f[1] * w0[g][1].z + f[2] * w0[g][2].z + f[3] * w0[g][3].z;
+          rv.w = f[0] * w0[g][0].w + f[1] * w0[g][1].w + f[2] * w0[g][2].w + f[3] * w0[g][3].w;
+        } else {
+          rv = *reinterpret_cast<const float4*>(a.h + (size_t)r * CH_BN + colof(g));
+        }
+        x[rb][4 * g] = (acc[rb][4 * g] + bv.x) + rv.x;
+        x[rb][4 * g + 1] = (acc[rb][4 * g + 1] + bv.y) + rv.y;
+        x[rb][4 * g + 2] = (acc[rb][4 * g + 2] + bv.z) + rv.z;
+        x[rb][4 * g + 3] = (acc[rb][4 * g + 3] + bv.w) + rv.w;
+      }
+    }
+  }
+  layernorm(a.ln1);  // its barriers: every wave is past its GEMM reads of the planes
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      put4(32 * rb + l32, colof(g), make_float4(x[rb][4 * g], x[rb][4 * g + 1], x[rb][4 * g + 2], x[rb][4 * g + 3]));
+  __syncthreads();
+  // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
+  gemm();
+  if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 bv = *reinterpret_cast<const float4*>(a.b2 + colof(g));
+      const float4 h1 = get4(32 * rb + l32, colof(g));
+      x[rb][4 * g] = h1.x + tanh_rat(acc[rb][4 * g] + bv.x);
+      x[rb][4 * g + 1] = h1.y + tanh_rat(acc[rb][4 * g + 1] + bv.y);
+      x[rb][4 * g + 2] = h1.z + tanh_rat(acc[rb][4 * g + 2] + bv.z);
+      x[rb][4 * g + 3] = h1.w + tanh_rat(acc[rb][4 * g + 3] + bv.w);
+    }
+  layernorm(a.ln2);
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = row0 + 32 * rb + l32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 y = make_float4(x[rb][4 * g], x[rb][4 * g + 1], x[rb][4 * g + 2], x[rb][4 * g + 3]);
+      if (a.Wp3) put4(32 * rb + l32, colof(g), y);
+      if (r < rows) *reinterpret_cast<float4*>(a.h + (size_t)r * CH_BN + colof(g)) = y;
+    }
+  }
+  if (!a.Wp3) return;
+  __syncthreads();
+  // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
+  for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
+    if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
+    gemm();
+    if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = row0 + 32 * rb + l32;
+      if (r >= rows || (ABLS == 2 && acc[rb][0] != 1234.5f)) continue;
+      float* yr = a.Y3 + (size_t)r * a.ldy3;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = col0 + colof(g);
+        if (c + 3 < a.n3) {
+          const float4 bv = *reinterpret_cast<const float4*>(a.b3 + c);
+          *reinterpret_cast<float4*>(yr + c) = make_float4(acc[rb][4 * g] + bv.x, acc[rb][4 * g + 1] + bv.y,
+                                                           acc[rb][4 * g + 2] + bv.z, acc[rb][4 * g + 3] + bv.w);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < a.n3) yr[c + e] = acc[rb][4 * g + e] + a.b3[c + e];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 int x6_plane_rows(int ncols) { return round_up(ncols, kRowPad) + kRowPad; }
@@ -2155,8 +2454,18 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
                      const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s) {
   ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, feat};
-  ensure_smem(chain_x6_kernel, CH_SMEM);
-  hipLaunchKernelGGL(chain_x6_kernel, dim3((rows + CH_BM - 1) / CH_BM), dim3(768), CH_SMEM, s, a);
+  static const int form = [] {  // DH_CHAIN=2: the LDS-ring form; 3, 4: ablations (tools only)
+    const char* e = std::getenv("DH_CHAIN");
+    return e ? e[0] - '0' : 1;
+  }();
+  if (form == 2) {
+    ensure_smem(chain_x6_kernel, CH_SMEM);
+    hipLaunchKernelGGL(chain_x6_kernel, dim3((rows + CH_BM - 1) / CH_BM), dim3(768), CH_SMEM, s, a);
+  } else {
+    auto k = form == 3 ? chain_x6s_kernel<1> : form == 4 ? chain_x6s_kernel<2> : chain_x6s_kernel<0>;
+    ensure_smem(k, CS_SMEM);
+    hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
+  }
 }
 
 }  // namespace dh

@@ -198,9 +198,9 @@ def test_gemm_x6_layernorm_fused(cuda, mode, nw, rows):
 @pytest.mark.parametrize("n3", [0, 768, 192, 18])
 @pytest.mark.parametrize("rows", [96, 1000, 24576, 40960])
 def test_chain_x6_matches_separate_kernels(cuda, n3, rows):
-    """The chained log-psi layer tail (one launch: LN1 GEMM, LN2 GEMM, next linear map) is
-    bitwise the separate split-bf16 kernels (same k order, splits, LayerNorm statistics),
-    and within f32 of the float64 layer."""
+    """The chained log-psi layer tail (one launch: LN1 GEMM, LN2 GEMM, next linear map)
+    against the separate split-bf16 kernels (same products in the same k order; the
+    LayerNorm sums in another order: f32 rounding) and the float64 layer."""
     lib = _lib.load()
     g = torch.Generator(device="cpu").manual_seed(rows + n3)
     K = D = 256
@@ -235,10 +235,11 @@ def test_chain_x6_matches_separate_kernels(cuda, n3, rows):
     assert lib.dh_debug_chain_x6(_p(X1), _p(Wp1), ldp, _p(b1), _p(ln1), _p(Wp2), ldp, _p(b2), _p(ln2), _p(Wp3), ldp3,
                                  _p(b3), n3, _p(Y_ch), ldy, _p(h_ch), rows, _stream()) == 0
     torch.cuda.synchronize()
-    assert torch.equal(h_ch[:rows], h_sep[:rows])
+    assert (h_ch[:rows] - h_sep[:rows]).abs().max().item() < 4e-6
     assert torch.equal(h_ch[rows:], h0[rows:])  # padding rows untouched
     if n3:
-        assert torch.equal(Y_ch[:rows, :n3], Y_sep[:rows, :n3])
+        ys = Y_sep[:rows, :n3]
+        assert (Y_ch[:rows, :n3] - ys).abs().max().item() < 4e-6 * max(1.0, ys.abs().max().item())
     # float64 layer
     def ln(y, p):
         mu = y.mean(-1, keepdim=True)
