@@ -613,8 +613,11 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
   const bool h_feat = C == 1 && fused && x6 && ln_fused;
   // log psi, split-bf16, D = 256: each layer's tail (Wo Wl + LN1, Wm + LN2) and the next
-  // linear map (the next layer's q|k|v, or the orbitals) run as ONE launch (chain_x6_kernel)
-  const bool chain = C == 1 && x6 && ln_fused && D == 256 && chain_x6_enabled();
+  // linear map (the next layer's q|k|v, or the orbitals) run as ONE launch (chain_x6s_kernel).
+  // Its 96-row tiles suit up to ~64K walker rows (C2 24576: 256 tiles, C4 40960: 427); at
+  // C5 (81920 rows, 2320 orbital columns) the separate GEMMs with 128-row LayerNorm tiles are
+  // faster (102.6 vs 103.6 ms per step, tools/chain_bench.py, profiles/)
+  const bool chain = C == 1 && x6 && ln_fused && D == 256 && rows < 65536 && chain_x6_enabled();
   {
     const bool wq = fold && !fused;
     PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));

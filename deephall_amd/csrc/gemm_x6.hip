@@ -2063,7 +2063,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     for (int rb = 0; rb < RB; ++rb) {
       const int r = row0 + 32 * rb + l32;
       float f[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.feat.W0) {
+      if (a.feat.W0 && r < rows) {  // geo holds exactly rows entries
         const float4 gq = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
         f[0] = gq.y;
         f[1] = gq.x * gq.w;
@@ -2080,7 +2080,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
           rv.z = f[0] * w0[g][0].z + f[1] * w0[g][1].z + f[2] * w0[g][2].z + f[3] * w0[g][3].z;
           rv.w = f[0] * w0[g][0].w + f[1] * w0[g][1].w + f[2] * w0[g][2].w + f[3] * w0[g][3].w;
         } else {
-          rv = *reinterpret_cast<const float4*>(a.h + (size_t)r * CH_BN + colof(g));
+          rv = *reinterpret_cast<const float4*>(a.h + (size_t)r * CH_BN + colof(g));  // h padded to 768 rows
         }
         x[rb][4 * g] = (acc[rb][4 * g] + bv.x) + rv.x;
         x[rb][4 * g + 1] = (acc[rb][4 * g + 1] + bv.y) + rv.y;

@@ -54,12 +54,13 @@ def init_distributed(backend: str | None = None):
 def init_guess(key: Key, batch: int, nelec: int, device=None, walker_offset: int = 0, network=None) -> torch.Tensor:
     """train.py:40-54 on the device: theta = arccos U(-1,1), phi = U(-pi,pi)."""
     device = torch.device(device or "cuda")
-    if network is None:
+    spec = getattr(network, "spec", None)
+    if spec is None or sum(spec.nspins) != nelec:
+        # the device kernel draws nelec = the handle's electron count per walker: a handle of
+        # another size (e.g. one_rdm's single r' per walker) would write past x
         from .networks.psiformer import NetworkSpec
 
         spec = NetworkSpec(nspins=(nelec, 0), flux=2, ndets=1, num_heads=1, heads_dim=4, num_layers=0)
-    else:
-        spec = network.spec
     h = get_handle(spec, device)
     x = torch.empty(batch, nelec, 2, dtype=torch.float32, device=device)
     _lib.check(h.lib.dh_init_walkers(h.h, _ptr(x), batch, int(key.seed), int(walker_offset), _stream(device)))

@@ -148,6 +148,8 @@ def test_driver_on_a_checkpoint(cuda, tmp_path):
     assert out["pair_corr"].shape == (40,) and torch.isfinite(out["pair_corr"]).all()
     out, vals = evaluate(DeepHallAdaptor(), one_rdm.DEFAULT, ckpt, steps, burn_in=3)
     assert vals["one_rdm"].shape == (steps, 7, 7) and out["diagonal"].shape == (7,)
-    assert abs(out["trace"].real.item() - 3.0) < 1.0  # a few-step estimate of N
+    # trace = N x the state's weight in the lowest Landau level (<= N; the Jastrow factor of
+    # a 3-iteration network moves some weight out); a 4-step, 64-walker estimate is noisy
+    assert torch.isfinite(out["trace"]).all() and 0.3 < out["trace"].real.item() < 4.0
     out, vals = evaluate(DeepHallAdaptor(), overlap.DEFAULT, ckpt, steps, burn_in=3)
     assert 0.0 <= out["overlap"].item() <= 1.0 + 1e-6
