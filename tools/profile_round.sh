@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 B="bench.py --steps 5 --warmup 1 --burn-in 0 --no-cpu-baseline --no-components"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/bench_under_rocprof.json
-R="--kernel-include-regex gemm --output-format csv"
+R="--kernel-include-regex (gemm|chain) --output-format csv"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE $R -d $OUT/fetch -o f -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-components --no-kernel-events > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE $R -d $OUT/write -o w -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-components --no-kernel-events > /dev/null
 python3 tools/pmc_traffic.py $(find $OUT/fetch -name "*counter_collection.csv") $(find $OUT/write -name "*counter_collection.csv") > $OUT/gemm_traffic.json
