@@ -48,7 +48,8 @@ struct Work {
 
 Work carve(const Dims& d, int nw, int C, void* base) {
   const int rows = nw * d.N * C;
-  const size_t rp = (size_t)round_up(std::max(rows, 1), kWalkerRowPad);
+  // + CH_BM rows: the channel chain's electron-aligned 96-row tiles read past the last row
+  const size_t rp = (size_t)round_up(std::max(rows, 1) + 96, kWalkerRowPad);
   const size_t nh = align64(rp * d.D);
   const size_t nqkv = align64(rp * (size_t)std::max(3 * d.D, d.ld_orb));
   Work w{};
@@ -618,6 +619,9 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // C5 (81920 rows, 2320 orbital columns) the separate GEMMs with 128-row LayerNorm tiles are
   // faster (102.6 vs 103.6 ms per step, tools/chain_bench.py, profiles/)
   const bool chain = C == 1 && x6 && ln_fused && D == 256 && rows < 65536 && chain_x6_enabled();
+  // local energy, split-bf16, D = 256: the channel layer tail (Wo Wl + LN_ch, Wm + tanh_ch +
+  // LN_ch) and the next linear map in ONE launch per layer (chain_ch_kernel)
+  const bool chain_ch = C > 1 && x6 && nt && D == 256 && chain_ch_supported(d.N);
   {
     const bool wq = fold && !fused;
     PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
@@ -626,11 +630,21 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0 && !chain) gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
+    if (l > 0 && !chain && !chain_ch)
+      gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     {
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
+    }
+    if (chain_ch) {
+      const bool last = l + 1 == d.L;
+      const int n3 = last ? d.orb_cols : 3 * D;
+      PROF(PK_GEMM + PK_CH, 2.0 * R * DD * (2.0 * DD + n3), f4 * (3.0 * R * DD + R * n3 + 2.0 * DD * DD + DD * n3));
+      launch_chain_ch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
+                      last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
+                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, w.geo, s);
+      continue;
     }
     if (chain) {
       const bool last = l + 1 == d.L;
@@ -673,7 +687,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  if (!chain || d.L == 0)
+  if ((!chain && !chain_ch) || d.L == 0)
     gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }

@@ -111,6 +111,13 @@ struct X6Feat {
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
 bool chain_x6_enabled();
+// Channel-row (C > 1) layer tail in one launch (gemm_x6.hip chain_ch_kernel; D = 256):
+// h = LN_ch(h + X1 Wol + b1); h = LN_ch(h + tanh_ch(h Wm + b2)); Y3 = h W3 (+ b3) if Wp3.
+bool chain_ch_supported(int N);
+void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, const float* geo,
+                     hipStream_t s);
 // Log-psi layer tail in one launch (D = K = 256): h1 = LN1(h + X1 Wol + b1) (feature
 // residual when feat.W0), h = LN2(h1 + tanh(h1 Wm + b2)), then Y3 = h W3 + b3 if Wp3.
 void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,

@@ -29,6 +29,7 @@
 
 #include "dh_internal.h"
 #include "device_common.h"
+#include "ln_ch_wave.h"
 
 namespace dh {
 
@@ -2150,6 +2151,250 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
 }
 
+
+// ---- chained channel layer tail ----------------------------------------------------------------
+// The local energy's (2N+5)-channel rows (C > 1) through one layer tail per launch:
+//   P1  h1 = LN_ch(h + o Wol + bol)             (layernorm.hip mode 0)  -> h (in place)
+//   P2  h  = LN_ch(h1 + tanh_ch(h1 Wm + bm))     (mode 1)                -> h
+//   P3  Y3 = h W3 (+ b3 on value rows)           the next layer's q|k|v, or the orbitals
+// as chain_x6s_kernel (activations as LDS bf16 planes split once, weights streamed L2 ->
+// registers, 8 waves of 32 columns x 96 rows), with tiles of E = 96 / C WHOLE electrons
+// (RV = E C rows; C2: 5 electrons = 85 of the 96 MFMA rows), so every electron's channel
+// rows are in one tile: after each GEMM pass the tile goes to an f32 scratch over the
+// planes and one wave per electron runs layernorm.hip's wave algebra (ln_ch_wave) on it.
+// The t / z intermediates never reach HBM; h1 round-trips through h (the mode-1 residual).
+template <int N>
+__global__ __launch_bounds__(512) void chain_ch_kernel(ChainArgs a) {
+  constexpr int ABLS = 0, C = 2 * N + 5, E = CH_BM / C, RV = E * C, LSF = CH_LS;
+  constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  int bid = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
+    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
+  }
+  const int row0 = bid * RV, rows = a.rows;  // tiles of E whole electrons (RV rows)
+  // plane p, tile row r, column c (bf16 units)
+  auto pl = [&](int p, int r, int c) __attribute__((always_inline)) {
+    return smem + (size_t)p * CS_PLANE + (size_t)r * (LSP * 2) + c * 2;
+  };
+  // write 4 consecutive f32 of row r, columns c..c+3 as their three bf16 terms
+  auto put4 = [&](int r, int c, const float4& x) __attribute__((always_inline)) {
+    uint2 h, m, l;
+    split4(x, h, m, l);
+    *reinterpret_cast<uint2*>(pl(0, r, c)) = h;
+    *reinterpret_cast<uint2*>(pl(1, r, c)) = m;
+    *reinterpret_cast<uint2*>(pl(2, r, c)) = l;
+  };
+  // the f32 value back from the planes (exact: a = a0 + a1 + a2 with no rounding)
+  auto get4 = [&](int r, int c) __attribute__((always_inline)) {
+    const uint2 h = *reinterpret_cast<const uint2*>(pl(0, r, c));
+    const uint2 m = *reinterpret_cast<const uint2*>(pl(1, r, c));
+    const uint2 l = *reinterpret_cast<const uint2*>(pl(2, r, c));
+    return make_float4((lo_f(h.x) + lo_f(m.x)) + lo_f(l.x), (hi_f(h.x) + hi_f(m.x)) + hi_f(l.x),
+                       (lo_f(h.y) + lo_f(m.y)) + lo_f(l.y), (hi_f(h.y) + hi_f(m.y)) + hi_f(l.y));
+  };
+
+  // ---- one GEMM pass: acc[rb] = rows 32 rb + l32 x columns col0 + 32 wid + ..  The weight
+  // fragments of its first PD k-tiles are requested by prefetch() beforehand, ahead of the
+  // previous pass's epilogue: its stores then do not sit in front of them in vmcnt's queue
+  f32x16 acc[RB];
+  bf16x8 bq[PD][3];
+  const uint16_t* wr = nullptr;
+  size_t plane = 0;
+  auto prefetch = [&](const uint16_t* Wp, int ldp, int col0) __attribute__((always_inline)) {
+    plane = (size_t)ldp * CH_K;
+    wr = Wp + (size_t)(col0 + 32 * wid + l32) * CH_K + 8 * lh;
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
+  };
+  auto gemm = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[rb][e] = 0.f;
+    // A fragments of k-tile kt (rows 32 rb + l32, k = 16 kt + 8 lh ..), read one k-tile ahead
+    bf16x8 ca[RB][3];
+    auto lda = [&](int kt, bf16x8(&d)[RB][3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          d[rb][p] = *reinterpret_cast<const bf16x8*>(pl(p, 32 * rb + l32, 16 * kt + 8 * lh));
+    };
+    lda(0, ca);
+#pragma unroll
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16x8 b0 = bq[kt % PD][0], b1 = bq[kt % PD][1], b2 = bq[kt % PD][2];
+      if (kt + PD < nk) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bq[kt % PD][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + (ABLS ? 0 : 16 * (kt + PD)));
+      }
+      bf16x8 cn[RB][3];
+      if (kt + 1 < nk) lda(kt + 1, cn);
+      // keep the prefetches where they are: the scheduler would sink each load to just
+      // before its first use and expose the L2 / LDS latency
+      __builtin_amdgcn_sched_barrier(0);
+      // product-major over the three row blocks: consecutive MFMAs are independent
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][2], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, ca[rb][0], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][1], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][1], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][0], acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][0], acc[rb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) ca[rb][p] = cn[rb][p];
+      }
+    }
+  };
+  // MFMA layout: reg 4 g + e of acc[rb] = tile row 32 rb + l32, column 32 wid + 8 g + 4 lh + e
+  auto colof = [&](int g) __attribute__((always_inline)) { return 32 * wid + 8 * g + 4 * lh; };
+  float* scr = reinterpret_cast<float*>(smem);  // [96][LSF] f32 scratch over the planes
+  // acc (+ bias on the value-channel rows, + residual R) -> scratch, MFMA layout
+  auto acc_to_scr = [&](const float* bias, const float* R) __attribute__((always_inline)) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 32 * rb + l32, rg = row0 + r;
+      const bool val = (r % C) == 0, own = r < RV && rg < rows;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float4 v = make_float4(acc[rb][4 * g], acc[rb][4 * g + 1], acc[rb][4 * g + 2], acc[rb][4 * g + 3]);
+        if (val) {
+          const float4 bv = *reinterpret_cast<const float4*>(bias + colof(g));
+          v.x += bv.x;
+          v.y += bv.y;
+          v.z += bv.z;
+          v.w += bv.w;
+        }
+        if (R && own) {
+          const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)rg * CH_BN + colof(g));
+          v.x += rv.x;
+          v.y += rv.y;
+          v.z += rv.z;
+          v.w += rv.w;
+        }
+        *reinterpret_cast<float4*>(scr + r * LSF + colof(g)) = v;
+      }
+    }
+  };
+  // scratch (f32) -> planes, in place: every thread holds its 12 float4 across the barrier
+  auto scr_to_planes = [&]() __attribute__((always_inline)) {
+    float4 v[CH_BM * (CH_BN / 4) / 512];
+#pragma unroll
+    for (int i = 0; i < CH_BM * (CH_BN / 4) / 512; ++i) {
+      const int q = tid + 512 * i, r = q / (CH_BN / 4), c = 4 * (q % (CH_BN / 4));
+      v[i] = *reinterpret_cast<const float4*>(scr + r * LSF + c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < CH_BM * (CH_BN / 4) / 512; ++i) {
+      const int q = tid + 512 * i, r = q / (CH_BN / 4), c = 4 * (q % (CH_BN / 4));
+      put4(r, c, v[i]);
+    }
+    __syncthreads();
+  };
+  const int eg = row0 / C + wid;                       // this wave's electron (LayerNorm stage)
+  const bool lnw = wid < E && (eg + 1) * C <= rows;   // wave-uniform
+  const int sub4 = 4 * lane;
+  auto srow = [&](int c) __attribute__((always_inline)) {
+    return reinterpret_cast<float4*>(scr + (wid * C + c) * LSF + sub4);
+  };
+  auto grow = [&](int c) __attribute__((always_inline)) {
+    return reinterpret_cast<float4*>(a.h + ((size_t)eg * C + c) * CH_BN + sub4);
+  };
+
+  // ---- P1 prologue: o rows -> planes (each element split once)
+  prefetch(a.Wp1, a.ldp1, 0);
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
+#pragma unroll 4
+    for (int i = tid; i < CH_BM * (CH_K / 4); i += 512) {
+      const int r = i / (CH_K / 4), c = 4 * (i % (CH_K / 4));
+      put4(r, c, src[i]);
+    }
+    __syncthreads();
+  }
+  // ---- P1: h1 = LN_ch(o Wol + bol + h) -> h (global, in place) and the planes
+  gemm();
+  __syncthreads();  // every wave is past its GEMM reads of the planes
+  acc_to_scr(a.b1, a.h);
+  __syncthreads();
+  if (lnw)
+    ln_ch_wave<N>(
+        0, [&](int c) { return *srow(c); }, [&](int c) { return *srow(c); },
+        [&](int c, const float4& v) {
+          *srow(c) = v;
+          *grow(c) = v;
+        },
+        a.ln1, a.feat.geo, eg / N, lane);
+  __syncthreads();
+  // (the next pass's weights are requested here, not before the epilogue: held across the
+  // LayerNorm and the plane conversion they push the kernel past 256 VGPRs)
+  prefetch(a.Wp2, a.ldp2, 0);
+  scr_to_planes();
+  // ---- P2: h2 = LN_ch(h1 + tanh_ch(h1 Wm + bm)) -> h (and the planes for P3)
+  gemm();
+  __syncthreads();
+  acc_to_scr(a.b2, nullptr);
+  __syncthreads();
+  if (lnw)
+    ln_ch_wave<N>(
+        1, [&](int c) { return *srow(c); }, [&](int c) { return *grow(c); },
+        [&](int c, const float4& v) {
+          *grow(c) = v;
+          *srow(c) = v;
+        },
+        a.ln2, a.feat.geo, eg / N, lane);
+  if (!a.Wp3) return;
+  __syncthreads();
+  if (32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
+  scr_to_planes();
+  // ---- P3: Y3 = h2 W3 (+ b3 on the value rows), 256-column passes, MFMA-layout stores
+  for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
+    if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
+    gemm();
+    if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 32 * rb + l32, rg = row0 + r;
+      if (r >= RV || rg >= rows) continue;
+      const bool val = (r % C) == 0;
+      float* yr = a.Y3 + (size_t)rg * a.ldy3;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = col0 + colof(g);
+        if (c + 3 < a.n3) {
+          const float4 bv = val ? *reinterpret_cast<const float4*>(a.b3 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(yr + c) = make_float4(acc[rb][4 * g] + bv.x, acc[rb][4 * g + 1] + bv.y,
+                                                           acc[rb][4 * g + 2] + bv.z, acc[rb][4 * g + 3] + bv.w);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < a.n3) yr[c + e] = acc[rb][4 * g + e] + (val ? a.b3[c + e] : 0.f);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 int x6_plane_rows(int ncols) { return round_up(ncols, kRowPad) + kRowPad; }
@@ -2466,6 +2711,39 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
     ensure_smem(k, CS_SMEM);
     hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
   }
+}
+
+// Chained channel layer tail (chain_ch_kernel above): rows = B N C channel rows; X1 and h
+// readable to round_up(rows + 96, kWalkerRowPad) rows (carve).  N = 3, 6 (C1, C2).
+// Opt-in (DH_CHAIN_CH=1): correct (the parity suite passes with it), but SLOWER than the
+// persistent 256-row channel GEMMs + separate LayerNorm at C2 (E_L 5.08 -> 5.71 ms): its
+// 96-row tiles stream the weights per 85 useful rows (~15 GB of L2 -> CU traffic per step
+// against x6q's LDS-shared 256-row tiles), which costs more than the LayerNorm passes save.
+bool chain_ch_supported(int N) {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_CHAIN_CH");
+    return e && e[0] == '1';
+  }();
+  return on && (N == 3 || N == 6);
+}
+
+void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
+                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, const float* geo,
+                     hipStream_t s) {
+  X6Feat f{};
+  f.geo = geo;
+  f.N = N;
+  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, f};
+  auto go = [&](auto kern, int C) {
+    const int RV = (CH_BM / C) * C;
+    ensure_smem(kern, CS_SMEM);
+    hipLaunchKernelGGL(kern, dim3((rows + RV - 1) / RV), dim3(512), CS_SMEM, s, a);
+  };
+  if (N == 3)
+    go(chain_ch_kernel<3>, 11);
+  else
+    go(chain_ch_kernel<6>, 17);
 }
 
 }  // namespace dh

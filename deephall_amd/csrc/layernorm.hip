@@ -19,6 +19,7 @@
 
 #include "dh_internal.h"
 #include "device_common.h"
+#include "ln_ch_wave.h"
 
 namespace dh {
 namespace {
@@ -253,138 +254,16 @@ __global__ __launch_bounds__(256) void layernorm_ch_wave_kernel(const float* X, 
                                                                 const float* __restrict__ ln,
                                                                 const float* __restrict__ geo, float* h, int ne,
                                                                 int mode) {
-  constexpr int T = 2 * N, C = 2 * N + 5, D = 256;
+  constexpr int C = 2 * N + 5, D = 256;
   const int e = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // walker*N + electron
   if (e >= ne) return;
   const int lane = threadIdx.x & 63;
-  const int b = e / N;
-  // flow coefficients alpha[k][t] (uniform over the wave)
-  float al[3][T];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
-    al[0][2 * i] = -g.z;
-    al[1][2 * i] = g.w;
-    al[2][2 * i] = 0.f;
-    al[0][2 * i + 1] = -(g.y * g.w);
-    al[1][2 * i + 1] = -(g.y * g.z);
-    al[2][2 * i + 1] = g.x;
-  }
   const size_t r4 = (size_t)e * C * (D / 4) + lane;  // float4 index of (row e*C, column quad lane)
-  float4 z[C];
-  if (mode == 0) {
-#pragma unroll
-    for (int c = 0; c < C; ++c) z[c] = reinterpret_cast<const float4*>(X)[r4 + c * (D / 4)];
-  } else {
-    // y = h + tanh_ch(Z), componentwise; Z streamed channel by channel
-    const float4 z0 = reinterpret_cast<const float4*>(Z)[r4];
-    float4 y0, d1, d2;
-#define DH_TANH_D(F)          \
-  y0.F = tanhf(z0.F);         \
-  d1.F = 1.f - y0.F * y0.F;   \
-  d2.F = -2.f * y0.F * d1.F;
-    DH_TANH_D(x) DH_TANH_D(y) DH_TANH_D(z) DH_TANH_D(w)
-#undef DH_TANH_D
-    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f), uz[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) uz[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    z[0] = reinterpret_cast<const float4*>(h)[r4];
-    z[0].x += y0.x;
-    z[0].y += y0.y;
-    z[0].z += y0.z;
-    z[0].w += y0.w;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float4 zt = reinterpret_cast<const float4*>(Z)[r4 + (1 + t) * (D / 4)];
-      z[1 + t] = reinterpret_cast<const float4*>(h)[r4 + (1 + t) * (D / 4)];
-#define DH_TANH_T(F)                        \
-  sq.F = fmaf(zt.F, zt.F, sq.F);            \
-  uz[0].F = fmaf(al[0][t], zt.F, uz[0].F);  \
-  uz[1].F = fmaf(al[1][t], zt.F, uz[1].F);  \
-  uz[2].F = fmaf(al[2][t], zt.F, uz[2].F);  \
-  z[1 + t].F = fmaf(d1.F, zt.F, z[1 + t].F);
-      DH_TANH_T(x) DH_TANH_T(y) DH_TANH_T(z) DH_TANH_T(w)
-#undef DH_TANH_T
-    }
-#pragma unroll
-    for (int c = 1 + T; c < C; ++c) {
-      const float4 zc = reinterpret_cast<const float4*>(Z)[r4 + c * (D / 4)];
-      z[c] = reinterpret_cast<const float4*>(h)[r4 + c * (D / 4)];
-      const float4 w = (c == 1 + T) ? sq : uz[c - 2 - T];
-      const bool L = c == 1 + T;
-#define DH_TANH_O(F) z[c].F += d1.F * zc.F + d2.F * (L ? w.F : w.F * w.F);
-      DH_TANH_O(x) DH_TANH_O(y) DH_TANH_O(z) DH_TANH_O(w)
-#undef DH_TANH_O
-    }
-  }
-  // channel means, centre
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float mu = wave_sum((z[c].x + z[c].y) + (z[c].z + z[c].w)) * (1.f / D);
-    z[c].x -= mu;
-    z[c].y -= mu;
-    z[c].z -= mu;
-    z[c].w -= mu;
-  }
-  float4 u[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    u[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      u[k].x = fmaf(al[k][t], z[1 + t].x, u[k].x);
-      u[k].y = fmaf(al[k][t], z[1 + t].y, u[k].y);
-      u[k].z = fmaf(al[k][t], z[1 + t].z, u[k].z);
-      u[k].w = fmaf(al[k][t], z[1 + t].w, u[k].w);
-    }
-  }
-  auto dot4 = [](const float4& a, const float4& b) { return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w); };
-  float p[C], q[T], uu[3];
-#pragma unroll
-  for (int c = 0; c < C; ++c) p[c] = wave_sum(dot4(z[0], z[c])) * (1.f / D);
-#pragma unroll
-  for (int t = 0; t < T; ++t) q[t] = wave_sum(dot4(z[1 + t], z[1 + t])) * (1.f / D);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) uu[k] = wave_sum(dot4(u[k], u[k])) * (1.f / D);
-  const float s = 1.f / sqrtf(p[0] + 1e-5f), s2 = s * s;
-  float at[T], cl = 0.f;
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    at[t] = s2 * p[1 + t];
-    cl += 3.f * at[t] * at[t] - s2 * q[t];
-  }
-  float au[3], cs[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    au[k] = 0.f;
-#pragma unroll
-    for (int t = 0; t < T; ++t) au[k] = fmaf(al[k][t], at[t], au[k]);
-    cs[k] = 3.f * au[k] * au[k] - s2 * uu[k];
-  }
-  const float4 g = reinterpret_cast<const float4*>(ln)[lane];
-  const float4 bb = reinterpret_cast<const float4*>(ln + D)[lane];
-  float4* out = reinterpret_cast<float4*>(h) + r4;
-  const float aL = s2 * p[1 + T];
-#define DH_LN_OUT(F)                                                                             \
-  {                                                                                              \
-    const float z0 = z[0].F, gs = g.F * s;                                                       \
-    float sat = 0.f;                                                                             \
-    _Pragma("unroll") for (int t = 0; t < T; ++t) sat = fmaf(at[t], z[1 + t].F, sat);            \
-    o0.F = g.F * (s * z0) + bb.F;                                                                \
-    _Pragma("unroll") for (int t = 0; t < T; ++t) ot[t].F = gs * (z[1 + t].F - at[t] * z0);      \
-    oL.F = gs * (z[1 + T].F - aL * z0 - 2.f * sat + cl * z0);                                    \
-    _Pragma("unroll") for (int k = 0; k < 3; ++k) oS[k].F =                                      \
-        gs * (z[2 + T + k].F - s2 * p[2 + T + k] * z0 - 2.f * au[k] * u[k].F + cs[k] * z0);     \
-  }
-  float4 o0, ot[T], oL, oS[3];
-  DH_LN_OUT(x) DH_LN_OUT(y) DH_LN_OUT(z) DH_LN_OUT(w)
-#undef DH_LN_OUT
-  out[0] = o0;
-#pragma unroll
-  for (int t = 0; t < T; ++t) out[(1 + t) * (D / 4)] = ot[t];
-  out[(1 + T) * (D / 4)] = oL;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) out[(2 + T + k) * (D / 4)] = oS[k];
+  const float4* src = reinterpret_cast<const float4*>(mode == 0 ? X : Z);
+  float4* hv = reinterpret_cast<float4*>(h);
+  ln_ch_wave<N>(
+      mode, [&](int c) { return src[r4 + c * (D / 4)]; }, [&](int c) { return hv[r4 + c * (D / 4)]; },
+      [&](int c, const float4& v) { hv[r4 + c * (D / 4)] = v; }, ln, geo, e / N, lane);
 }
 
 // Channel rows for large N (C = 2N+5 up to 45), D = 256: FOUR WAVES per (walker,
