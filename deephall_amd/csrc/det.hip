@@ -97,22 +97,23 @@ __device__ inline cf env_flow2(const cf& e0, const cf& dth, const cf& d2th, floa
   return r;
 }
 
-// wave 0 finds the pivot row (first max of |re|+|im| in column p, rows >= p)
-__device__ inline void find_pivot(const cf* A, int lda, int N, int p, int* piv) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+// the first `width` threads (a wave, or a half-wave per walker) find the pivot row (first
+// max of |re|+|im| in column p, rows >= p)
+__device__ inline void find_pivot(const cf* A, int lda, int N, int p, int* piv, int tid, int width) {
+  if (tid < width) {
+    const int lane = tid;
     float best = -1.f;
     int bi = N;
-    for (int r = p + lane; r < N; r += 64) {
+    for (int r = p + lane; r < N; r += width) {
       const float v = cabs1(A[r * lda + p]);
       if (v > best) {
         best = v;
         bi = r;
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
+    for (int o = width >> 1; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, width);
+      const int oi = __shfl_xor(bi, o, width);
       if (ob > best || (ob == best && oi < bi)) {
         best = ob;
         bi = oi;
@@ -126,12 +127,14 @@ __device__ inline void find_pivot(const cf* A, int lda, int N, int p, int* piv) 
 //   gj = true : Gauss-Jordan on an augmented [A | I] (ncol = 2N): right block -> A^-1
 //   gj = false: LU (rows below the pivot only) — determinant only
 // Accumulates log det into logdet (complex, phase unwrapped).  Uses __syncthreads.
-__device__ void eliminate(cf* A, int lda, int N, int ncol, bool gj, cf* fac, int* piv, cf* logdet) {
-  const int tid = threadIdx.x, nt = blockDim.x;
+// tid / nt: this walker's threads (default the whole block; det_value's half-wave form
+// passes its 32 lanes and width 32 for the pivot search).
+__device__ void eliminate(cf* A, int lda, int N, int ncol, bool gj, cf* fac, int* piv, cf* logdet,
+                          int tid = threadIdx.x, int nt = blockDim.x, int width = 64) {
   if (tid == 0) *logdet = cf{0.f, 0.f};
   __syncthreads();
   for (int p = 0; p < N; ++p) {
-    find_pivot(A, lda, N, p, piv);
+    find_pivot(A, lda, N, p, piv, tid, width);
     __syncthreads();
     const int pr = *piv;
     if (pr != p) {
@@ -186,18 +189,27 @@ __device__ inline double jastrow_pair(double r, double al, double cst, double* f
 // (G = 64 / N lane groups, u < MGV, all loads of a row in flight at once, one wave load
 // instruction covering G consecutive harmonics = 4 G N contiguous bytes), groups combined
 // with shuffles.
-template <int MGV>
+// HW (MGV = 0 only): two walkers per wave, one per 32-lane half (per-walker LDS regions of
+// `per` floats): the serial parts (pivot search, log det, Jastrow reduction) then serve two
+// walkers per instruction.
+template <int MGV, bool HW = false>
 __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                  const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
-                                 int N, int n_up, int M, int K) {
-  extern __shared__ float sm_raw[];
+                                 int N, int n_up, int M, int K, int nw, int per) {
+  static_assert(!HW || MGV == 0, "half-wave form: serial contraction only");
+  extern __shared__ float sm_all[];
+  const int half = HW ? (int)(threadIdx.x >> 5) : 0;
+  float* sm_raw = sm_all + half * per;
   cf* E0 = reinterpret_cast<cf*>(sm_raw);  // [N][M]
   cf* A = E0 + N * M;                      // [N][N]
   cf* fac = A + N * N;                     // [N]
   cf* ld = fac + N;                        // [K] log dets
   cf* logdet = ld + K;
   int* piv = reinterpret_cast<int*>(logdet + 1);
-  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int bw = HW ? 2 * (int)blockIdx.x + half : (int)blockIdx.x;
+  const bool live = bw < nw;
+  const int b = live ? bw : nw - 1;  // a dead half repeats the last walker, writes nothing
+  const int tid = HW ? (int)(threadIdx.x & 31) : (int)threadIdx.x, nt = HW ? 32 : 64, width = HW ? 32 : 64;
   double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] unit vectors (double: close pairs)
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
@@ -227,7 +239,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
       double f1, f2;
       Jw += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
     }
-    for (int o = 32; o > 0; o >>= 1) Jw += __shfl_xor(Jw, o, 64);
+    for (int o = width >> 1; o > 0; o >>= 1) Jw += __shfl_xor(Jw, o, width);
   }
   const int G = 64 / N, gj = tid % N, gg = tid / N, NK = N * K, MNK = M * NK;
   for (int k = 0; k < K; ++k) {
@@ -263,11 +275,11 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
       if (gg == 0) A[i * N + gj] = cf{re, im};
     }
     __syncthreads();
-    eliminate(A, N, N, N, false, fac, piv, logdet);
+    eliminate(A, N, N, N, false, fac, piv, logdet, tid, nt, width);
     if (tid == 0) ld[k] = *logdet;
     __syncthreads();
   }
-  if (tid == 0) {
+  if (tid == 0 && live) {
     // log-sum-exp over determinants (psiformer.py:74-76)
     float lmax = -INFINITY;
     for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, ld[k].re);
@@ -1243,15 +1255,28 @@ void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStrea
                      d.interaction);
 }
 
+// DH_DET_HW=0 keeps one walker per wave in det_value (A/B measurements)
+static bool det_value_hw() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_DET_HW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s) {
-  const size_t bytes = (size_t)(2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2) * sizeof(float);
+  const int per = (2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2 + 3) & ~3;  // floats
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M,
-                       d.K);
+    hipLaunchKernelGGL(kern, dim3(nw), dim3(64), (size_t)per * sizeof(float), s, F, d.ld_orb, x, jastrow, norm,
+                       logpsi, d.N, d.n_up, d.M, d.K, nw, per);
   };
   const int mgv = (d.M + 64 / d.N - 1) / (64 / d.N);  // harmonics per lane
-  if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
+  if (mgv <= 2 && d.N * d.N <= 64 && det_value_hw()) {
+    // two walkers per wave (C2, M = 16, N = 6)
+    hipLaunchKernelGGL((det_value_kernel<0, true>), dim3((nw + 1) / 2), dim3(64), (size_t)2 * per * sizeof(float), s, F,
+                       d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per);
+  } else if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
     go(det_value_kernel<0>);
   else if (mgv <= 4)
     go(det_value_kernel<4>);
