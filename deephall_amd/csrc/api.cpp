@@ -581,7 +581,9 @@ size_t dh_workspace_bytes(const dh_handle* h, int batch, int op) {
 namespace {
 
 // One Psiformer pass over nw walkers with C channels; leaves orbital features in w.F.
-int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s) {
+// geo_ready: w.geo already holds the walkers' geometry (written by the MCMC proposal); the
+// input kernel is then skipped when the geometry is all it would write.
+int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false) {
   const Dims& d = h->d;
   const Params& P = h->p;
   const int rows = nw * d.N * C;
@@ -624,9 +626,11 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   const bool chain_ch = C > 1 && x6 && nt && D == 256 && chain_ch_supported(d.N);
   {
     const bool wq = fold && !fused;
-    PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
-    launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, h_feat ? nullptr : w.h,
-                 wq ? w.qkv : nullptr, w.geo, nw, C, s);
+    if (!(geo_ready && h_feat && !wq)) {
+      PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
+      launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, h_feat ? nullptr : w.h,
+                   wq ? w.qkv : nullptr, w.geo, nw, C, s);
+    }
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
@@ -700,14 +704,15 @@ int ensure_expo(dh_handle* h) {
 }
 
 // log psi of nw walkers into logpsi [nw][2]: the Psiformer pass or the Laughlin kernel
-int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logpsi, hipStream_t s) {
+int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logpsi, hipStream_t s,
+               bool geo_ready = false) {
   if (h->laughlin) {
     if (int rc = ensure_expo(h)) return rc;
     PROF(PK_DET_VALUE, 0.0, 8.0 * nw * h->d.N);
     launch_laughlin(h->d, x, h->expo, logpsi, nullptr, nullptr, nw, s);
     return check_launch();
   }
-  if (int rc = run_trunk(h, x, nw, 1, w, s)) return rc;
+  if (int rc = run_trunk(h, x, nw, 1, w, s, geo_ready)) return rc;
   {
     PROF(PK_DET_VALUE, 0.0, 4.0 * nw * h->d.N * h->d.ld_orb);
     launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s);
@@ -749,18 +754,26 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
   if (int rc = value_pass(h, x, B, w, w.logpsi, s)) return rc;
   launch_lp_from_logpsi(w.logpsi, lp, n_accept, B, s);
   const size_t nstride = (size_t)B * (2 * d.N + 1);
+  // step st: accept of st - 1 and the proposal of st in one launch (which also writes the
+  // proposal's geometry, so the trunk skips its input kernel); the last accept alone
+  const bool geo = !h->laughlin;
   for (int st = 0; st < steps; ++st) {
     const float* nz = noise ? noise + st * nstride : nullptr;
     const uint64_t step = counter + (uint64_t)st;
     {
       PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
-      launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s);
+      if (st == 0)
+        launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s, geo ? w.geo : nullptr);
+      else
+        launch_accept_propose(d, x, w.x2, geo ? w.geo : nullptr, lp, w.logpsi, n_accept, B, width, seed, step - 1,
+                              walker_offset, noise ? noise + (st - 1) * nstride : nullptr, nz, s);
     }
-    if (int rc = value_pass(h, w.x2, B, w, w.logpsi, s)) return rc;
-    {
-      PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
-      launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, step, walker_offset, nz, 0, s);
-    }
+    if (int rc = value_pass(h, w.x2, B, w, w.logpsi, s, geo)) return rc;
+  }
+  if (steps > 0) {
+    PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
+    launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, counter + (uint64_t)(steps - 1), walker_offset,
+                  noise ? noise + (steps - 1) * nstride : nullptr, 0, s);
   }
   return check_launch();
 }

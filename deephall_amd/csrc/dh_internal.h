@@ -134,8 +134,13 @@ void launch_transpose(const float* src, int ld_src, int rows, int cols, float* d
 void launch_input(const Dims& d, const float* x, const float* W0, const float* W0qkv, const float* bqkv, float* h,
                   float* qkv, float* geo, int nw, int C, hipStream_t s);
 // Proposal (mcmc.py:67-102): x2 = sph_sampling(x, noise).
+// geo (optional): the proposal's geometry (sin/cos of the f32 angles, as input_kernel).
 void launch_propose(const Dims& d, const float* x, float* x2, int nw, float width, uint64_t seed, uint64_t step,
-                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s);
+                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s, float* geo = nullptr);
+// accept of `step` + proposal of `step + 1` (and its geometry) in one launch.
+void launch_accept_propose(const Dims& d, float* x, float* x2, float* geo, float* lp, const float* logpsi2,
+                           int32_t* n_acc, int nw, float width, uint64_t seed, uint64_t step, int64_t walker_offset,
+                           const float* noise, const float* noise2, hipStream_t s);
 void launch_init_walkers(const Dims& d, float* x, int nw, uint64_t seed, int64_t walker_offset, hipStream_t s);
 
 // attention.hip: channel self-attention for all heads.

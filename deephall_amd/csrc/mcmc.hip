@@ -10,6 +10,8 @@
 // Random numbers: Philox4x32-10 keyed by the seed, counter (lane, global walker,
 // step) — see device_common.h — or injected arrays [B][2N+1] per step
 // (normals[N], phi uniforms[N], accept uniform) for parity tests.
+#include <algorithm>
+
 #include "dh_internal.h"
 #include "device_common.h"
 
@@ -18,11 +20,11 @@ namespace {
 
 constexpr int kPurposeMcmc = 0, kPurposeInit = 1;
 
-__global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ x2, int nw, int N, float width,
-                               uint64_t seed, uint64_t step, int64_t woff, const float* __restrict__ noise) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nw * N) return;
-  const int b = e / N, i = e % N;
+// One electron's move: (th, ph) -> x2[e] (and its geometry sin/cos of the stored f32
+// angles into geo[e], as input_kernel computes it, when geo is given).
+__device__ __forceinline__ void propose_one(float th_f, float ph_f, float* __restrict__ x2, float* __restrict__ geo,
+                                            int e, int b, int i, int N, float width, uint64_t seed, uint64_t step,
+                                            int64_t woff, const float* __restrict__ noise) {
   float xi, up;
   if (noise) {
     xi = noise[(size_t)b * (2 * N + 1) + i];
@@ -36,7 +38,7 @@ __global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ 
   // f32): phi = sign(y) arccos(x / sin theta) loses ~eps / |sin phi| near phi = 0, pi in
   // f32 (the reference's own f32 result is off by up to ~3e-4 rad there); in double the
   // stored walker is the correctly rounded exact move.  ~20 double ops per electron.
-  const double th = x[2 * e], ph = x[2 * e + 1];
+  const double th = th_f, ph = ph_f;
   const double thp = atan((double)xi * (double)width);
   const double php = (double)up * 2.0 * M_PI;
   double stp, ctp, spp, cpp, st, ct, sp, cp;
@@ -57,6 +59,64 @@ __global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ 
   const float phn = (float)(sgn * acos(qc));
   x2[2 * e] = thn;
   x2[2 * e + 1] = phn;
+  if (geo) {
+    float gst, gct, gsp, gcp;
+    sincosf(thn, &gst, &gct);
+    sincosf(phn, &gsp, &gcp);
+    *reinterpret_cast<float4*>(geo + 4 * (size_t)e) = make_float4(gst, gct, gsp, gcp);
+  }
+}
+
+__global__ void propose_kernel(const float* __restrict__ x, float* __restrict__ x2, float* __restrict__ geo, int nw,
+                               int N, float width, uint64_t seed, uint64_t step, int64_t woff,
+                               const float* __restrict__ noise) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nw * N) return;
+  propose_one(x[2 * e], x[2 * e + 1], x2, geo, e, e / N, e % N, N, width, seed, step, woff, noise);
+}
+
+// accept_kernel for step `step` and the proposal of step `step + 1` in one launch: thread
+// per electron; every thread of a walker recomputes the walker's accept decision (same
+// random number, same inputs), moves only its own electron, and proposes its next move
+// from the result (noise2: the next step's injected noise).
+__global__ void accept_propose_kernel(float* __restrict__ x, float* __restrict__ x2, float* __restrict__ geo,
+                                      float* __restrict__ lp, const float* __restrict__ logpsi2,
+                                      int32_t* __restrict__ nacc, int nw, int N, float width, uint64_t seed,
+                                      uint64_t step, int64_t woff, const float* __restrict__ noise,
+                                      const float* __restrict__ noise2) {
+  // blocks hold whole walkers (blockDim = N x walkers per block), so the barrier below
+  // orders every read of lp[b] before its rewrite
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool on = e < nw * N;
+  const int b = e / N, i = e % N;
+  bool cond = false;
+  float lp2 = 0.f, th = 0.f, ph = 0.f;
+  if (on) {
+    float u;
+    if (noise) {
+      u = noise[(size_t)b * (2 * N + 1) + 2 * N];
+    } else {
+      u32x4 r = dh_random(seed, kPurposeMcmc, (uint32_t)N, (uint64_t)(woff + b), step);
+      u = u01(r.x);
+    }
+    lp2 = 2.f * logpsi2[2 * b];
+    cond = (lp2 - lp[b]) > logf(u);
+    th = x[2 * e];
+    ph = x[2 * e + 1];
+    if (cond) {
+      th = x2[2 * e];
+      ph = x2[2 * e + 1];
+      x[2 * e] = th;
+      x[2 * e + 1] = ph;
+    }
+  }
+  __syncthreads();
+  if (!on) return;
+  if (cond && i == 0) {
+    lp[b] = lp2;
+    nacc[b] += 1;
+  }
+  propose_one(th, ph, x2, geo, e, b, i, N, width, seed, step + 1, woff, noise2);
 }
 
 __global__ void accept_kernel(float* __restrict__ x, const float* __restrict__ x2, float* __restrict__ lp,
@@ -101,11 +161,19 @@ __global__ void init_kernel(float* __restrict__ x, int nw, int N, uint64_t seed,
 }  // namespace
 
 void launch_propose(const Dims& d, const float* x, float* x2, int nw, float width, uint64_t seed, uint64_t step,
-                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s) {
+                    int64_t walker_offset, const float* noise, int noise_stride, hipStream_t s, float* geo) {
   (void)noise_stride;
   const int n = nw * d.N;
-  hipLaunchKernelGGL(propose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, x2, nw, d.N, width, seed, step,
+  hipLaunchKernelGGL(propose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, x2, geo, nw, d.N, width, seed, step,
                      walker_offset, noise);
+}
+
+void launch_accept_propose(const Dims& d, float* x, float* x2, float* geo, float* lp, const float* logpsi2,
+                           int32_t* n_acc, int nw, float width, uint64_t seed, uint64_t step, int64_t walker_offset,
+                           const float* noise, const float* noise2, hipStream_t s) {
+  const int wpb = std::max(1, 256 / d.N);  // whole walkers per block
+  hipLaunchKernelGGL(accept_propose_kernel, dim3((nw + wpb - 1) / wpb), dim3(wpb * d.N), 0, s, x, x2, geo, lp,
+                     logpsi2, n_acc, nw, d.N, width, seed, step, walker_offset, noise, noise2);
 }
 
 void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_acc,
