@@ -640,7 +640,7 @@ struct FeatW {
 };
 
 template <int N, bool FEAT>
-__global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restrict__ qkv,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 : (N <= 12 ? 2 : 1)))) void attention_wave_kernel(const float* __restrict__ qkv,
                                                             const float* __restrict__ geo, float* __restrict__ o,
                                                             int H, const float* __restrict__ W0qkv,
                                                             const float* __restrict__ bqkv, int n_up) {
@@ -864,6 +864,18 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
         v0r[j] = VR ? v0reg[VR ? j : 0] : v0[j * ld + lane];
         vcr[j] = VR ? vcreg[VR ? j : 0] : vc[j * ld + lane];
       }
+      // flow channels: Vu_k[j] (this lane's column) once per channel, not once per (i, j)
+      // (FEAT: g_k(j) . Wv from the geometry; else the running sums, k selected once)
+      float vuj[N];
+      if (!tang && k >= 0) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          if constexpr (FEAT)
+            vuj[j] = FeatW::dot(gflow(k, j), fw.wv);
+          else
+            vuj[j] = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         float acc = 0.f, acc2 = 0.f;
@@ -891,16 +903,7 @@ __global__ __launch_bounds__(64) void attention_wave_kernel(const float* __restr
         } else {
           float a2 = 0.f;
 #pragma unroll
-          for (int j = 0; j < N; ++j) {
-            float vu;
-            if constexpr (FEAT) {
-              vu = FeatW::dot(gflow(k, j), fw.wv);
-            } else {
-              // rVu[k][j] with a runtime k: select without dynamic register indexing
-              vu = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
-            }
-            a2 = fmaf(Au[k * nn + i * N + j], vu, a2);
-          }
+          for (int j = 0; j < N; ++j) a2 = fmaf(Au[k * nn + i * N + j], vuj[j], a2);
           acc = fmaf(2.f, a2, acc);
         }
         obase[(size_t)(i * C + c) * D] = acc;
