@@ -49,6 +49,10 @@ EXPORTS = [
     "dh_potential",
     "dh_histograms",
     "dh_monopole_orbitals",
+    "dh_mh_init",
+    "dh_mh_propose",
+    "dh_mh_accept",
+    "dh_kinetic_from_derivatives",
     "dh_debug_trunk",
     "dh_debug_gemm",
     "dh_debug_gemm_ln",
@@ -171,6 +175,14 @@ def load(path: Path | str | None = None):
     lib.dh_grad_cotangent.restype = i32
     lib.dh_adam_update.argtypes = [vp, vp, vp, vp, sz, f32, f32, f32, f32, i32, vp]
     lib.dh_adam_update.restype = i32
+    lib.dh_mh_init.argtypes = [vp, vp, vp, i32, vp]
+    lib.dh_mh_init.restype = i32
+    lib.dh_mh_propose.argtypes = [vp, vp, i32, i32, f32, u64, u64, i64, vp, vp]
+    lib.dh_mh_propose.restype = i32
+    lib.dh_mh_accept.argtypes = [vp, vp, vp, vp, vp, i32, i32, u64, u64, i64, vp, vp]
+    lib.dh_mh_accept.restype = i32
+    lib.dh_kinetic_from_derivatives.argtypes = [vp, vp, vp, i32, i32, C.c_double, C.c_double, vp, vp, vp]
+    lib.dh_kinetic_from_derivatives.restype = i32
     lib.dh_profile_enable.argtypes = [vp, i32]
     lib.dh_profile_enable.restype = i32
     lib.dh_profile_read.argtypes = [vp, C.POINTER(C.c_double), i32]

@@ -1179,6 +1179,41 @@ int dh_monopole_orbitals(const float* points, int n, int flux, float* out, void*
   return check_launch();
 }
 
+// ---- log psi supplied by the caller (arbitrary callables, mcmc.py:105 / hamiltonian.py:83) ----
+
+int dh_mh_init(const float* logpsi, float* lp, int32_t* n_accept, int B, void* stream) {
+  if (!logpsi || !lp || !n_accept || B < 1) return fail(DH_EINVAL, "bad arguments");
+  launch_lp_from_logpsi(logpsi, lp, n_accept, B, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_mh_propose(const float* x, float* x2, int B, int nelec, float width, uint64_t seed, uint64_t step,
+                  int64_t walker_offset, const float* noise, void* stream) {
+  if (!x || !x2 || B < 1 || nelec < 1 || x == x2) return fail(DH_EINVAL, "bad arguments");
+  Dims d{};
+  d.N = nelec;
+  launch_propose(d, x, x2, B, width, seed, step, walker_offset, noise, 0, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_mh_accept(float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_accept, int B, int nelec,
+                 uint64_t seed, uint64_t step, int64_t walker_offset, const float* noise, void* stream) {
+  if (!x || !x2 || !lp || !logpsi2 || !n_accept || B < 1 || nelec < 1) return fail(DH_EINVAL, "bad arguments");
+  Dims d{};
+  d.N = nelec;
+  launch_accept(d, x, x2, lp, logpsi2, n_accept, B, seed, step, walker_offset, noise, 0, (hipStream_t)stream);
+  return check_launch();
+}
+
+int dh_kinetic_from_derivatives(const double* x, const double* grad, const double* hess, int B, int nelec, double Q,
+                                double r, float* ke, float* mom, void* stream) {
+  if (!x || !grad || !hess || !ke || !mom || B < 1 || nelec < 1 || !(r > 0.0) || Q < 0.0)
+    return fail(DH_EINVAL, "bad arguments");
+  if (kinetic_assembly_lds_bytes(nelec) > 64 * 1024) return fail(DH_EINVAL, "nelec > 256");
+  launch_kinetic_assembly(x, grad, hess, B, nelec, Q, r, ke, mom, (hipStream_t)stream);
+  return check_launch();
+}
+
 int dh_init_walkers(dh_handle* h, float* x, int B, uint64_t seed, int64_t walker_offset, void* stream) {
   if (!h || !x || B < 1) return fail(DH_EINVAL, "bad arguments");
   launch_init_walkers(h->d, x, B, seed, walker_offset, (hipStream_t)stream);

@@ -181,6 +181,11 @@ void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const fl
                    int noise_stride, hipStream_t s);
 void launch_lp_from_logpsi(const float* logpsi, float* lp, int32_t* n_acc, int nw, hipStream_t s);
 
+// kinetic.hip: KE / Lz / Lz^2 / L^2 of an arbitrary log psi from its derivatives
+size_t kinetic_assembly_lds_bytes(int N);
+void launch_kinetic_assembly(const double* x, const double* g, const double* H, int nw, int N, double Q, double r,
+                             float* ke, float* mom, hipStream_t s);
+
 // stats.hip
 void launch_stats(const float* e_l, const float* obs, const int32_t* n_acc, int B, int steps, int penalties,
                   float* out, hipStream_t s);

@@ -5,7 +5,9 @@
 reference differentiates ``f`` with ``jax.grad`` and two full ``jax.hessian``
 calls (hamiltonian.py:105-113); here the kernels propagate 2N+5 forward-mode
 channels through the network and assemble KE, Lz, Lz^2, L^2 and
-the potential in one native call (dh_local_energy).
+the potential in one native call (dh_local_energy).  Any other callable ``f`` (the
+reference's tests pass analytic Slater determinants) goes through generic.py:
+torch.func derivatives of the caller's function, HIP assembly of KE / L^2.
 """
 
 from __future__ import annotations
@@ -16,7 +18,7 @@ import torch
 
 from . import _lib
 from .config import InteractionType, System
-from .mcmc import resolve_network
+from .mcmc import native_network
 from .networks.psiformer import NetworkSpec, Psiformer, _ptr, _stream, get_handle
 
 DEFAULT_WORKSPACE_BYTES = 24 << 30
@@ -49,7 +51,11 @@ def _observables(e_l, obs):
 
 
 def local_energy(f, system: System):
-    net = resolve_network(f)
+    net = native_network(f)
+    if net is None:
+        from . import generic
+
+        return generic.local_energy(f, system)
     _check_system(net, system)
 
     def _e_l(params, data: torch.Tensor):
@@ -66,7 +72,11 @@ make_local_energy = local_energy
 
 def make_local_kinetic_energy(f, Q: float, r):
     """hamiltonian.py:83-172: returns ``ke(params, data) -> (KE complex [B], AngularMomenta)``."""
-    net = resolve_network(f)
+    net = native_network(f)
+    if net is None:
+        from . import generic
+
+        return generic.make_local_kinetic_energy(f, Q, r)
     if abs(2 * Q - net.spec.flux) > 1e-6:
         raise ValueError(f"Q={Q} does not match the network's flux {net.spec.flux}")
     r = float(r)

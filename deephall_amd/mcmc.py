@@ -24,8 +24,9 @@ from .networks.psiformer import Psiformer, _ptr, _stream
 from .random import Key
 
 
-def resolve_network(f) -> Psiformer:
-    """The MI355X kernels need the network itself, not an opaque callable."""
+def native_network(f) -> Psiformer | None:
+    """The network of this library behind ``f`` (itself, its bound .apply, or a function
+    carrying ``.network``), or None for any other callable."""
     if isinstance(f, Psiformer):
         return f
     owner = getattr(f, "__self__", None)
@@ -34,13 +35,28 @@ def resolve_network(f) -> Psiformer:
     net = getattr(f, "network", None)
     if isinstance(net, Psiformer):
         return net
-    raise TypeError(
-        "deephall_amd needs a Psiformer (or its bound .apply) — arbitrary Python callables cannot run on the HIP path"
-    )
+    return None
+
+
+def resolve_network(f) -> Psiformer:
+    """The network itself, for the paths that need its parameters (loss, training)."""
+    net = native_network(f)
+    if net is None:
+        raise TypeError("this path needs a deephall_amd network (Psiformer / Laughlin or its bound .apply)")
+    return net
 
 
 def make_mcmc_step(batch_network, batch_per_device: int, steps: int = 10):
-    net = resolve_network(batch_network)
+    """Native networks run the whole call in dh_mcmc_step; any other batched callable
+    ``batch_network(params, data[B, N, 2]) -> complex[B]`` goes through generic.py (its log
+    psi evaluated by the caller's code, proposal and accept in HIP on the same streams)."""
+    net = native_network(batch_network)
+    if net is None:
+        if not callable(batch_network):
+            raise TypeError("batch_network must be callable")
+        from . import generic
+
+        return generic.make_mcmc_step(batch_network, batch_per_device, steps)
 
     def mcmc_step(params, data: torch.Tensor, key: Key, width, *, noise=None, walker_offset=None, reduce=True):
         """Run ``steps`` MH moves in place.  Returns (data, pmove) with pmove a 0-d tensor.

@@ -244,6 +244,32 @@ int dh_histograms(const float* x, int B, int nelec, int density_bins, int pair_b
  * +-(1 - 1e-4) as there). */
 int dh_monopole_orbitals(const float* points, int n, int flux, float* out, void* stream);
 
+/* ---- log psi supplied by the caller: the arbitrary-callable boundary ---------------------
+ * The reference's make_mcmc_step(batch_network, ...) (mcmc.py:105-150) and
+ * make_local_kinetic_energy(f, Q, r) (hamiltonian.py:83-172) accept ANY log psi.  For one
+ * that is not a network of this library the caller evaluates log psi (and, for the energy,
+ * its derivatives) itself; these entry points do the rest on the device.
+ *
+ * MCMC with the same random streams as dh_mcmc_step (so a caller-evaluated network walks
+ * exactly as the native one):
+ *   dh_mh_init     lp[b] = 2 Re logpsi[b][0], n_accept[b] = 0           (mcmc.py:142)
+ *   dh_mh_propose  x2 = sph_sampling(x) for step `step` = counter + s    (mcmc.py:67-102)
+ *   dh_mh_accept   accept/select with logpsi2[B][2] = log psi(x2) (re, im): x, lp, n_accept
+ *                  updated where 2 Re log psi(x2) - lp > log U             (mcmc.py:25-64)
+ * noise: NULL or this step's injected [B][2N+1] (dh_mcmc_step layout).
+ *
+ * dh_kinetic_from_derivatives: KE (complex) and Lz, Lz^2, L^2 from x[B][N][2], the complex
+ * first derivatives grad[B][N][2][2] (d/dtheta, d/dphi; re, im) and complex Hessian
+ * hess[B][N][2][N][2][2] of log psi, all double; Q monopole strength, r radius; nelec <= 256.
+ * Out: ke[B][2] (re, im), mom[B][3] (Lz, Lz^2, L^2). */
+int dh_mh_init(const float* logpsi, float* lp, int32_t* n_accept, int B, void* stream);
+int dh_mh_propose(const float* x, float* x2, int B, int nelec, float width, uint64_t seed, uint64_t step,
+                  int64_t walker_offset, const float* noise, void* stream);
+int dh_mh_accept(float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_accept, int B, int nelec,
+                 uint64_t seed, uint64_t step, int64_t walker_offset, const float* noise, void* stream);
+int dh_kinetic_from_derivatives(const double* x, const double* grad, const double* hess, int B, int nelec, double Q,
+                                double r, float* ke, float* mom, void* stream);
+
 /* Kernel timing with HIP events on the launch stream (bench / roofline).
  * dh_profile_enable(h, 1) starts recording every kernel launch of this handle;
  * dh_profile_read fills out[k*4 + {0,1,2,3}] = {launches, total ms, algorithmic
