@@ -114,7 +114,7 @@ def make_mcmc_step(batch_network, batch_per_device: int, steps: int = 10):
 def update_mcmc_width(t, width, adapt_frequency, pmove, pmoves, pmove_max=0.55, pmove_min=0.5):
     """mcmc.py:153-186."""
     t_since = t % adapt_frequency
-    pmoves[t_since] = float(pmove.reshape(-1)[0].item() if isinstance(pmove, torch.Tensor) else pmove)
+    pmoves[t_since] = float(pmove.item() if isinstance(pmove, torch.Tensor) else pmove)
     if t > 0 and t_since == 0:
         if np.mean(pmoves) > pmove_max:
             width *= 1.1

@@ -19,6 +19,7 @@ it on the device) and manages the per-device handle and workspace.
 from __future__ import annotations
 
 import ctypes as C
+import functools
 import os
 import math
 from dataclasses import dataclass
@@ -232,12 +233,54 @@ def ref_offsets(spec: NetworkSpec) -> list:
     return offs
 
 
+@functools.lru_cache(maxsize=None)
+def _leaf_offsets(spec: NetworkSpec) -> tuple:
+    """((name, byte offset into the flat tree), ...) in dh_ref_layout order."""
+    return tuple((name, 4 * o) for name, o in zip(param_shapes(spec), ref_offsets(spec)))
+
+
 class ParamTree(dict):
     """{Flax path: tensor} whose tensors are views into ONE flat float32 buffer in the
     dh_ref_layout order (``.flat``).  Optimizers update ``.flat`` in place; the kernels
-    upload it as is."""
+    upload it as is.  Replacing a leaf goes through item assignment (``tree[name] = t``),
+    which the tree counts, so the view check runs once per mutation, not once per call
+    (it sits between a step's host sync and its first launch)."""
 
     flat: torch.Tensor
+    _mut = 0
+    _checked = None
+
+    def _touch(self):
+        self._mut += 1
+        self._checked = None
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        self._touch()
+
+    def __delitem__(self, k):
+        super().__delitem__(k)
+        self._touch()
+
+    def update(self, *a, **kw):
+        super().update(*a, **kw)
+        self._touch()
+
+    def pop(self, *a):
+        self._touch()
+        return super().pop(*a)
+
+    def popitem(self):
+        self._touch()
+        return super().popitem()
+
+    def setdefault(self, *a):
+        self._touch()
+        return super().setdefault(*a)
+
+    def clear(self):
+        super().clear()
+        self._touch()
 
     @classmethod
     def zeros(cls, spec: NetworkSpec, device) -> "ParamTree":
@@ -255,10 +298,14 @@ class ParamTree(dict):
         if flat is None:
             return False
         base = flat.data_ptr()
-        for (name, _), o in zip(param_shapes(spec).items(), ref_offsets(spec)):
+        sig = (spec, base, self._mut)
+        if self._checked == sig:
+            return True
+        for name, off in _leaf_offsets(spec):
             v = self.get(name)
-            if v is None or v.data_ptr() != base + 4 * o or not v.is_contiguous():
+            if v is None or v.data_ptr() != base + off or not v.is_contiguous():
                 return False
+        self._checked = sig
         return True
 
 
