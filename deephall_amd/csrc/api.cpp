@@ -636,7 +636,10 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     const LayerParams& lp = P.layer[l];
     if (l > 0 && !chain && !chain_ch)
       gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
-    {
+    // log psi, chain form: layer 1's attention runs in the chain kernel's prologue (its o
+    // never leaves the CU; attn_val.h)
+    const bool attn_in_chain = chain && fused && l == 0 && chain_attn_supported(d.N, d.H, d.dh);
+    if (!attn_in_chain) {
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
@@ -654,10 +657,15 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       const bool last = l + 1 == d.L;
       const int n3 = last ? d.orb_cols : 3 * D;
       PROF(PK_GEMM, 2.0 * R * DD * (2.0 * DD + n3), f4 * (2.0 * R * DD + R * n3 + 2.0 * DD * DD + DD * n3));
+      X6Feat feat{};
+      if (h_feat && l == 0) feat = X6Feat{P.W0, w.geo, d.N, d.n_up};
+      if (attn_in_chain) {
+        feat.W0qkv = P.W0qkv;
+        feat.bqkv = lp.bqkv;
+      }
       launch_chain_x6(w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
                       last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
-                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows,
-                      (h_feat && l == 0) ? X6Feat{P.W0, w.geo, d.N, d.n_up} : X6Feat{}, s);
+                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, feat, s);
       continue;
     }
     if (ln_fused) {

@@ -13,6 +13,7 @@
 // qkv rows are (walker, electron, channel); columns [q | k | v], head h at h*dh.
 #include "dh_internal.h"
 #include "device_common.h"
+#include "attn_val.h"
 
 namespace dh {
 namespace {
@@ -620,25 +621,6 @@ __device__ __forceinline__ float4 feature_channel(int c, int i, float4 g, float 
   return make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
 }
 
-// Per-lane slice of the folded layer-1 projection: column (h, lane) of q, k and v.
-struct FeatW {
-  float4 wq, wk, wv;
-  float bq, bk, bv;
-  __device__ void load(const float* W0qkv, const float* bqkv, int D, int col) {
-    const int ld = 3 * D;
-    wq = make_float4(W0qkv[col], W0qkv[ld + col], W0qkv[2 * ld + col], W0qkv[3 * ld + col]);
-    wk = make_float4(W0qkv[D + col], W0qkv[ld + D + col], W0qkv[2 * ld + D + col], W0qkv[3 * ld + D + col]);
-    wv = make_float4(W0qkv[2 * D + col], W0qkv[ld + 2 * D + col], W0qkv[2 * ld + 2 * D + col],
-                     W0qkv[3 * ld + 2 * D + col]);
-    bq = bqkv[col];
-    bk = bqkv[D + col];
-    bv = bqkv[2 * D + col];
-  }
-  __device__ __forceinline__ static float dot(float4 f, float4 w) {
-    return fmaf(f.x, w.x, fmaf(f.y, w.y, fmaf(f.z, w.z, f.w * w.w)));
-  }
-};
-
 template <int N, bool FEAT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 : (N <= 12 ? 2 : 1)))) void attention_wave_kernel(const float* __restrict__ qkv,
                                                             const float* __restrict__ geo, float* __restrict__ o,
@@ -954,82 +936,33 @@ __global__ __launch_bounds__(256) void attention_val_kernel(const float* __restr
                                                             const float* __restrict__ geo, float* __restrict__ o,
                                                             int H, int ntask, const float* __restrict__ W0qkv,
                                                             const float* __restrict__ bqkv, int n_up) {
-  constexpr int dh = 64, ld = 68, nn = N * N, PER = 2 * N * ld + nn;
+  constexpr int dh = 64, PER = attn_val_floats<N>();
   extern __shared__ float sm[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int task = blockIdx.x * 4 + w;
   if (task >= ntask) return;  // the whole wave leaves; nothing below synchronises waves
-  float* qs = sm + w * PER;
-  float* ks = qs + N * ld;
-  float* A = ks + N * ld;
+  float* qs = sm + w * PER;  // q, k rows and the weights (attn_val_core)
   const int b = task / H, h = task - (task / H) * H;
   const int D = H * dh;
-  float pq[N], pk[N], pv[N];
+  float pq[1][N], pk[1][N], pv[1][N];
   if constexpr (FEAT) {
     FeatW fw;
     fw.load(W0qkv, bqkv, D, h * dh + lane);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
-      const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (i < n_up) ? 1.f : -1.f);
-      pq[i] = FeatW::dot(f, fw.wq) + fw.bq;
-      pk[i] = FeatW::dot(f, fw.wk) + fw.bk;
-      pv[i] = FeatW::dot(f, fw.wv) + fw.bv;
-    }
+    feat_qkv<N>(fw, geo, b, n_up, pq[0], pk[0], pv[0]);
   } else {
     const float* base = qkv + (size_t)b * N * (3 * D) + h * dh + lane;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      pq[i] = base[(size_t)i * 3 * D];
-      pk[i] = base[(size_t)i * 3 * D + D];
-      pv[i] = base[(size_t)i * 3 * D + 2 * D];
+      pq[0][i] = base[(size_t)i * 3 * D];
+      pk[0][i] = base[(size_t)i * 3 * D + D];
+      pv[0][i] = base[(size_t)i * 3 * D + 2 * D];
     }
   }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    qs[i * ld + lane] = pq[i];
-    ks[i * ld + lane] = pk[i];
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int p = lane; p < 4 * nn; p += 64) {
-    const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
-    const float* x = qs + i * ld + 16 * qt;
-    const float* y = ks + j * ld + 16 * qt;
-    float sdot = 0.f;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float4 a = *reinterpret_cast<const float4*>(x + 4 * m);
-      const float4 c = *reinterpret_cast<const float4*>(y + 4 * m);
-      sdot = fmaf(a.x, c.x, fmaf(a.y, c.y, fmaf(a.z, c.z, fmaf(a.w, c.w, sdot))));
-    }
-    sdot += __shfl_xor(sdot, 1, 64);
-    sdot += __shfl_xor(sdot, 2, 64);
-    if (qt == 0) A[pair] = sdot * 0.125f;  // 1 / sqrt(64)
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (lane < N) {
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < N; ++j) m = fmaxf(m, A[lane * N + j]);
-    float e[N], ssum = 0.f;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      e[j] = expf(A[lane * N + j] - m);
-      ssum += e[j];
-    }
-    const float inv = 1.f / ssum;
-#pragma unroll
-    for (int j = 0; j < N; ++j) A[lane * N + j] = e[j] * inv;
-  }
-  __builtin_amdgcn_wave_barrier();
+  float out[1][N];
+  attn_val_core<N, 1>(pq, pk, pv, qs, lane, out);
   float* ob = o + (size_t)b * N * D + h * dh + lane;
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < N; ++j) acc = fmaf(A[i * N + j], pv[j], acc);
-    ob[(size_t)i * D] = acc;
-  }
+  for (int i = 0; i < N; ++i) ob[(size_t)i * D] = out[0][i];
 }
 
 template <int N>

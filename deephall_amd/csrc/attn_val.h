@@ -1,0 +1,112 @@
+// Self-attention of ONE (walker, head) on value rows (log psi, dh = 64; psiformer.py:44),
+// with layer 1's q|k|v formed from the K = 4 input features through the folded W0 Wqkv
+// (psiformer.py:51-60).  Shared by attention_val_kernel (attention.hip, o to HBM) and the
+// chained layer tail's prologue (gemm_x6.hip chain_x6s_kernel: layer 1's o straight into
+// its LDS planes), so both compute bit-identical outputs.
+#pragma once
+#include "device_common.h"
+
+namespace dh {
+
+// Per-lane slice of the folded layer-1 projection: column (h, lane) of q, k and v.
+struct FeatW {
+  float4 wq, wk, wv;
+  float bq, bk, bv;
+  __device__ void load(const float* W0qkv, const float* bqkv, int D, int col) {
+    const int ld = 3 * D;
+    wq = make_float4(W0qkv[col], W0qkv[ld + col], W0qkv[2 * ld + col], W0qkv[3 * ld + col]);
+    wk = make_float4(W0qkv[D + col], W0qkv[ld + D + col], W0qkv[2 * ld + D + col], W0qkv[3 * ld + D + col]);
+    wv = make_float4(W0qkv[2 * D + col], W0qkv[ld + 2 * D + col], W0qkv[2 * ld + 2 * D + col],
+                     W0qkv[3 * ld + 2 * D + col]);
+    bq = bqkv[col];
+    bk = bqkv[D + col];
+    bv = bqkv[2 * D + col];
+  }
+  __device__ __forceinline__ static float dot(float4 f, float4 w) {
+    return fmaf(f.x, w.x, fmaf(f.y, w.y, fmaf(f.z, w.z, f.w * w.w)));
+  }
+};
+
+// q|k|v rows of the N electrons of walker b at this lane's column of head h (fw)
+template <int N>
+__device__ __forceinline__ void feat_qkv(const FeatW& fw, const float* __restrict__ geo, int b, int n_up,
+                                         float (&pq)[N], float (&pk)[N], float (&pv)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+    const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (i < n_up) ? 1.f : -1.f);
+    pq[i] = FeatW::dot(f, fw.wq) + fw.bq;
+    pk[i] = FeatW::dot(f, fw.wk) + fw.bk;
+    pv[i] = FeatW::dot(f, fw.wv) + fw.bv;
+  }
+}
+
+// One wave, lane = feature column d of the head: softmax(q k^T / 8) v for the N electrons
+// of NT independent (walker, head) tasks, phase by phase so that their LDS round trips
+// overlap (each task's arithmetic is the NT = 1 one).  st: NT x attn_val_floats(N) floats
+// of wave-private LDS (per task q and k rows at stride 68, then the N x N weights).
+// out[t][i] = o of task t, electron i, column d.
+template <int N>
+__host__ __device__ constexpr int attn_val_floats() { return 2 * N * 68 + N * N; }
+
+template <int N, int NT>
+__device__ __forceinline__ void attn_val_core(const float (&pq)[NT][N], const float (&pk)[NT][N],
+                                              const float (&pv)[NT][N], float* st, int lane, float (&out)[NT][N]) {
+  constexpr int ld = 68, nn = N * N, PER = attn_val_floats<N>();
+  __builtin_amdgcn_wave_barrier();  // a previous call's readers of st (LDS ops of a wave run in order)
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      st[t * PER + i * ld + lane] = pq[t][i];
+      st[t * PER + N * ld + i * ld + lane] = pk[t][i];
+    }
+  __builtin_amdgcn_wave_barrier();
+  for (int p = lane; p < NT * 4 * nn; p += 64) {
+    const int t = p / (4 * nn), pp = p - t * (4 * nn);
+    const int pair = pp >> 2, qt = pp & 3, i = pair / N, j = pair - (pair / N) * N;
+    const float* x = st + t * PER + i * ld + 16 * qt;
+    const float* y = st + t * PER + N * ld + j * ld + 16 * qt;
+    float sdot = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 a = *reinterpret_cast<const float4*>(x + 4 * m);
+      const float4 c = *reinterpret_cast<const float4*>(y + 4 * m);
+      sdot = fmaf(a.x, c.x, fmaf(a.y, c.y, fmaf(a.z, c.z, fmaf(a.w, c.w, sdot))));
+    }
+    sdot += __shfl_xor(sdot, 1, 64);
+    sdot += __shfl_xor(sdot, 2, 64);
+    if (qt == 0) st[t * PER + 2 * N * ld + pair] = sdot * 0.125f;  // 1 / sqrt(64)
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < NT * N) {  // lane = (task, row)
+    const int t = lane / N, r = lane - t * N;
+    float* A = st + t * PER + 2 * N * ld + r * N;
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A[j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A[j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A[j] = e[j] * inv;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float* A = st + t * PER + 2 * N * ld;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(A[i * N + j], pv[t][j], acc);
+      out[t][i] = acc;
+    }
+  }
+}
+
+}  // namespace dh

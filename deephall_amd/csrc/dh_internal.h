@@ -107,10 +107,15 @@ struct X6Feat {
   const float* W0 = nullptr;
   const float* geo = nullptr;
   int N = 1, n_up = 0;
+  // launch_chain_x6 only: layer 1's attention formed in the chain prologue from the features
+  // (folded W0 Wqkv [4][3D], bqkv [3D]) instead of read from X1 (chain_attn_supported)
+  const float* W0qkv = nullptr;
+  const float* bqkv = nullptr;
 };
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
 bool chain_x6_enabled();
+bool chain_attn_supported(int N, int H, int dh);
 // Channel-row (C > 1) layer tail in one launch (gemm_x6.hip chain_ch_kernel; D = 256):
 // h = LN_ch(h + X1 Wol + b1); h = LN_ch(h + tanh_ch(h Wm + b2)); Y3 = h W3 (+ b3) if Wp3.
 bool chain_ch_supported(int N);

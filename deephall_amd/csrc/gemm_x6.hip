@@ -27,6 +27,7 @@
 // swizzled by (row>>2)&3 (16 lanes of a ds_read_b128 pass hit 16 distinct bank groups).
 #include <cstdlib>
 
+#include "attn_val.h"
 #include "dh_internal.h"
 #include "device_common.h"
 #include "ln_ch_wave.h"
@@ -1887,7 +1888,12 @@ __device__ __forceinline__ void split4(const float4& x, uint2& h, uint2& m, uint
   l = make_uint2(Lv[0], Lv[1]);
 }
 
-template <int ABLS = 0>  // ABLS (tools only): 1 weight fragments from one k-tile (L1-resident); 2 no P3 stores
+// NA > 0: layer 1 with its attention fused (X1 unused): the prologue forms o of the tile's
+// 96 / NA walkers itself (attn_val.h, bit-identical to attention_val_kernel<NA, true>): wave
+// w takes head w % 4 for walkers 48 / NA * (w / 4) .., two walkers per attn_val_core call
+// so their LDS round trips overlap, staging q / k in LDS that the planes
+// overwrite afterwards, the o values held in registers (48 per lane) until every wave is done.
+template <int ABLS = 0, int NA = 0>  // ABLS (tools only): 1 weight fragments from one k-tile (L1-resident); 2 no P3 stores
 __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
   extern __shared__ float4 smem4[];
@@ -2039,8 +2045,58 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   };
 
   // ---- P1 prologue: o rows -> planes (each element split once)
-  prefetch(a.Wp1, a.ldp1, 0);
-  {
+  if constexpr (NA > 0) {
+    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_K == 256, "walker-aligned tiles, 4 heads x 2 wave groups");
+    constexpr int WPW = 48 / NA, PER = 2 * attn_val_floats<NA>();  // walkers per wave, staging floats
+    static_assert(WPW % 2 == 0, "walker pairs");
+    prefetch(a.Wp1, a.ldp1, 0);
+    float* qs = reinterpret_cast<float*>(smem) + wid * PER;
+    const int hd = wid & 3, wl0 = (wid >> 2) * WPW;  // head; first tile walker of this wave
+    FeatW fw;
+    fw.load(a.feat.W0qkv, a.feat.bqkv, CH_K, hd * 64 + lane);
+    float ov[WPW][NA];
+    // two walkers per attn_val_core call (their LDS round trips overlap); the wave-uniform
+    // guards also keep the scheduler from hoisting later walkers' loads (spills)
+#pragma unroll
+    for (int t = 0; t < WPW; t += 2) {
+      const int b = row0 / NA + wl0 + t;
+      if ((b + 2) * NA <= rows) {
+        float pq[2][NA], pk[2][NA], pv[2][NA];
+        feat_qkv<NA>(fw, a.feat.geo, b, a.feat.n_up, pq[0], pk[0], pv[0]);
+        feat_qkv<NA>(fw, a.feat.geo, b + 1, a.feat.n_up, pq[1], pk[1], pv[1]);
+        attn_val_core<NA, 2>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[2][NA]>(ov[t]));
+      } else {  // the batch ends inside this pair (last tile)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if ((b + u + 1) * NA <= rows) {
+            float pq[1][NA], pk[1][NA], pv[1][NA];
+            feat_qkv<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pq[0], pk[0], pv[0]);
+            attn_val_core<NA, 1>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
+          } else {
+#pragma unroll
+            for (int i = 0; i < NA; ++i) ov[t + u][i] = 0.f;
+          }
+        }
+      }
+    }
+    __syncthreads();  // the staging areas lie in the planes
+#pragma unroll
+    for (int t = 0; t < WPW; ++t)
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {  // one element: the three bf16 terms of split4
+        const float x = ov[t][i];
+        const uint32_t h2 = pk_bf16(x, 0.f);
+        const float rx = x - lo_f(h2);
+        const uint32_t m2 = pk_bf16(rx, 0.f);
+        const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
+        const int r = (wl0 + t) * NA + i, c = hd * 64 + lane;
+        *reinterpret_cast<uint16_t*>(pl(0, r, c)) = (uint16_t)h2;
+        *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
+        *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
+      }
+    __syncthreads();
+  } else {
+    prefetch(a.Wp1, a.ldp1, 0);
     const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
 #pragma unroll 4
     for (int i = tid; i < CH_BM * (CH_K / 4); i += 512) {
@@ -2708,9 +2764,30 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
     hipLaunchKernelGGL(chain_x6_kernel, dim3((rows + CH_BM - 1) / CH_BM), dim3(768), CH_SMEM, s, a);
   } else {
     auto k = form == 3 ? chain_x6s_kernel<1> : form == 4 ? chain_x6s_kernel<2> : chain_x6s_kernel<0>;
+    if (feat.W0qkv) {  // chain_attn_supported(feat.N, 4, 64) checked by the caller
+      switch (feat.N) {
+        case 2: k = chain_x6s_kernel<0, 2>; break;
+        case 3: k = chain_x6s_kernel<0, 3>; break;
+        case 4: k = chain_x6s_kernel<0, 4>; break;
+        case 6: k = chain_x6s_kernel<0, 6>; break;
+        default: k = chain_x6s_kernel<0, 8>; break;
+      }
+    }
     ensure_smem(k, CS_SMEM);
     hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
   }
+}
+
+// Layer 1's attention inside the chain prologue (chain_x6s_kernel<0, N>): walker-aligned
+// 96-row tiles, 4 heads of 64 (one per wave pair), the production x6s form.  DH_CHAIN_ATTN=0
+// keeps the separate attention_val_kernel launch (A/B measurements).
+bool chain_attn_supported(int N, int H, int dh) {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_CHAIN_ATTN");
+    const char* f = std::getenv("DH_CHAIN");
+    return !(e && e[0] == '0') && !(f && f[0] != '1');
+  }();
+  return on && H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8);
 }
 
 // Chained channel layer tail (chain_ch_kernel above): rows = B N C channel rows; X1 and h
