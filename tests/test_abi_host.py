@@ -158,3 +158,24 @@ def test_callable_boundary_routing_and_no_cpu_path():
                                torch.rand(2, 3, 2, dtype=torch.float64))
     assert g.shape == (2, 3, 2) and H.shape == (2, 3, 2, 3, 2)
     assert torch.allclose(H[:, 1, 0, 1, 1].real, torch.ones(2, dtype=torch.float64))
+
+
+def test_param_tree_view_check_tracks_mutations():
+    """ParamTree.is_packed_view caches its leaf walk per tree mutation (the check sits between
+    a step's host sync and its first launch): replacing a leaf through any dict mutator makes
+    the tree a non-packed view again; in-place leaf updates keep it packed."""
+    spec = NetworkSpec(nspins=(3, 0), flux=2, ndets=1, num_heads=4, heads_dim=64, num_layers=2)
+    t = init_params(spec, 0, "cpu")
+    assert t.is_packed_view(spec) and t.is_packed_view(spec)
+    name = next(iter(t))
+    t[name].add_(1.0)  # in place: still a view into flat
+    assert t.is_packed_view(spec)
+    t[name] = t[name].clone()
+    assert not t.is_packed_view(spec)
+    t2 = init_params(spec, 0, "cpu")
+    t2.update({name: t2[name].clone()})
+    assert not t2.is_packed_view(spec)
+    t3 = init_params(spec, 0, "cpu")
+    assert t3.is_packed_view(spec)
+    t3.pop(name)
+    assert not t3.is_packed_view(spec)
