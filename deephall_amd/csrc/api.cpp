@@ -583,8 +583,7 @@ namespace {
 // One Psiformer pass over nw walkers with C channels; leaves orbital features in w.F.
 // geo_ready: w.geo already holds the walkers' geometry (written by the MCMC proposal); the
 // input kernel is then skipped when the geometry is all it would write.
-int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false,
-              int* f_tiles = nullptr) {
+int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false) {
   const Dims& d = h->d;
   const Params& P = h->p;
   const int rows = nw * d.N * C;
@@ -702,7 +701,6 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   if ((!chain && !chain_ch) || d.L == 0)
     gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
-  if (f_tiles) *f_tiles = (chain && d.L > 0) ? (rows + 95) / 96 : 0;  // F written by the chain's 96-row tiles
   return check_launch();
 }
 
@@ -722,11 +720,10 @@ int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logps
     launch_laughlin(h->d, x, h->expo, logpsi, nullptr, nullptr, nw, s);
     return check_launch();
   }
-  int f_tiles = 0;
-  if (int rc = run_trunk(h, x, nw, 1, w, s, geo_ready, &f_tiles)) return rc;
+  if (int rc = run_trunk(h, x, nw, 1, w, s, geo_ready)) return rc;
   {
     PROF(PK_DET_VALUE, 0.0, 4.0 * nw * h->d.N * h->d.ld_orb);
-    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s, f_tiles);
+    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s);
   }
   return check_launch();
 }

@@ -192,13 +192,10 @@ __device__ inline double jastrow_pair(double r, double al, double cst, double* f
 // HW (MGV = 0 only): two walkers per wave, one per 32-lane half (per-walker LDS regions of
 // `per` floats): the serial parts (pivot search, log det, Jastrow reduction) then serve two
 // walkers per instruction.
-// xt > 0 (HW): F was just written by the chained layer tail's xt 96-row tiles, tile t by
-// XCD owner(t) (gemm_x6.hip's XCD-aware order); workgroup g runs on XCD g % 8 and takes a
-// walker pair of that XCD's tiles, so its orbital rows come from its own L2.
 template <int MGV, bool HW = false>
 __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                  const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
-                                 int N, int n_up, int M, int K, int nw, int per, int xt = 0) {
+                                 int N, int n_up, int M, int K, int nw, int per) {
   static_assert(!HW || MGV == 0, "half-wave form: serial contraction only");
   extern __shared__ float sm_all[];
   const int half = HW ? (int)(threadIdx.x >> 5) : 0;
@@ -209,16 +206,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
   cf* ld = fac + N;                        // [K] log dets
   cf* logdet = ld + K;
   int* piv = reinterpret_cast<int*>(logdet + 1);
-  int pair = blockIdx.x;
-  if (HW && xt > 0) {
-    const int xc = blockIdx.x & 7, slot = blockIdx.x >> 3, q = xt >> 3, r8 = xt & 7;
-    const int t0 = xc < r8 ? xc * (q + 1) : r8 * (q + 1) + (xc - r8) * q, ntl = q + (xc < r8 ? 1 : 0);
-    const int wpt = 96 / N;  // walkers per tile (even)
-    const int p0 = t0 * wpt / 2, p1 = (min((t0 + ntl) * wpt, nw) + 1) / 2;
-    if (p0 + slot >= p1) return;  // the whole (one-wave) workgroup
-    pair = p0 + slot;
-  }
-  const int bw = HW ? 2 * pair + half : (int)blockIdx.x;
+  const int bw = HW ? 2 * (int)blockIdx.x + half : (int)blockIdx.x;
   const bool live = bw < nw;
   const int b = live ? bw : nw - 1;  // a dead half repeats the last walker, writes nothing
   const int tid = HW ? (int)(threadIdx.x & 31) : (int)threadIdx.x, nt = HW ? 32 : 64, width = HW ? 32 : 64;
@@ -1277,23 +1265,17 @@ static bool det_value_hw() {
 }
 
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
-                      float* logpsi, int nw, hipStream_t s, int f_tiles) {
+                      float* logpsi, int nw, hipStream_t s) {
   const int per = (2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2 + 3) & ~3;  // floats
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(nw), dim3(64), (size_t)per * sizeof(float), s, F, d.ld_orb, x, jastrow, norm,
-                       logpsi, d.N, d.n_up, d.M, d.K, nw, per, 0);
+                       logpsi, d.N, d.n_up, d.M, d.K, nw, per);
   };
   const int mgv = (d.M + 64 / d.N - 1) / (64 / d.N);  // harmonics per lane
   if (mgv <= 2 && d.N * d.N <= 64 && det_value_hw()) {
-    // two walkers per wave (C2, M = 16, N = 6); with chain tiles, pairs grouped by the XCD
-    // that wrote their orbital rows
-    int grid = (nw + 1) / 2, xt = 0;
-    if (f_tiles > 0 && 96 % d.N == 0) {
-      xt = f_tiles;
-      grid = 8 * ((xt / 8 + (xt % 8 ? 1 : 0)) * (96 / d.N) / 2);
-    }
-    hipLaunchKernelGGL((det_value_kernel<0, true>), dim3(grid), dim3(64), (size_t)2 * per * sizeof(float), s, F,
-                       d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per, xt);
+    // two walkers per wave (C2, M = 16, N = 6)
+    hipLaunchKernelGGL((det_value_kernel<0, true>), dim3((nw + 1) / 2), dim3(64), (size_t)2 * per * sizeof(float), s, F,
+                       d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per);
   } else if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
     go(det_value_kernel<0>);
   else if (mgv <= 4)

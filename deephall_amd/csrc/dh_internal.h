@@ -169,7 +169,7 @@ void launch_layernorm(const Dims& d, const float* X, const float* Z, const float
 //   value mode (C == 1): logpsi[nw][2]
 //   energy mode (C == 2N+5): e_l[nw][2], obs[nw][8]
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
-                      float* logpsi, int nw, hipStream_t s, int f_tiles = 0);
+                      float* logpsi, int nw, hipStream_t s);
 // phic != nullptr (det_precontract(d)): the channel matrices are first contracted from F by
 // env_contract_kernel into phic [nw][K][C][N][N] complex, then assembled from there
 // NetObs estimators (netobs.hip): theta / pair-angle histograms, LLL monopole harmonics
