@@ -3,7 +3,7 @@
 from __future__ import annotations
 
 from ..config import Network, NetworkType, System
-from .laughlin import Laughlin
+from .laughlin import Laughlin, LaughlinQuasiparticle, laughlin_q1
 from .psiformer import Psiformer
 
 
@@ -11,6 +11,9 @@ def make_network(system: System, network: Network) -> Psiformer:
     Q = system.flux / 2
     ntype = str(getattr(network.type, "value", network.type))
     if ntype == NetworkType.laughlin.value:  # networks/__init__.py:24-27
+        if sum(system.nspins) == 2 * laughlin_q1(system.nspins, system.flux) + 2:  # quasiparticle filling
+            return LaughlinQuasiparticle(flux=system.flux, nspins=system.nspins, excitation_lz=system.lz_center,
+                                         system=system)
         return Laughlin(flux=system.flux, nspins=system.nspins, excitation_lz=system.lz_center, system=system)
     if ntype == NetworkType.psiformer.value:
         return Psiformer(
@@ -26,4 +29,4 @@ def make_network(system: System, network: Network) -> Psiformer:
     raise ValueError(f"unknown network type {network.type}")
 
 
-__all__ = ["make_network", "Psiformer", "Laughlin"]
+__all__ = ["make_network", "Psiformer", "Laughlin", "LaughlinQuasiparticle"]

@@ -7,7 +7,12 @@ It has no parameters: ``init`` returns an empty tree.  ``apply`` is batched log 
 (dh_logpsi); the MCMC step and the local energy run the HIP kernels of laughlin.hip
 through the same entry points as the Psiformer (make_mcmc_step, local_energy,
 make_local_kinetic_energy), with the full analytic Hessian in double precision.
-The quasiparticle state (laughlin.py:82-100) is rejected with a clear error.
+The quasiparticle state (N = 2 Q1 + 2, laughlin.py:82-100) is `LaughlinQuasiparticle`: its
+LLL-projected excited orbital depends on every electron through the Jastrow derivatives, so
+it is not a Slater determinant of one-electron orbitals and is evaluated as a log-psi
+callable (the reference's own form, slogdet of the orbital matrix) through the library's
+callable boundary (deephall_amd.generic: derivatives by torch.func, proposal / accept and
+the KE / Lz / L^2 assembly in HIP).
 """
 
 from __future__ import annotations
@@ -50,4 +55,57 @@ class Laughlin(Psiformer):
         raise TypeError("the Laughlin wavefunction has no parameters to differentiate")
 
 
-__all__ = ["Laughlin", "_lib", "_ptr", "_stream"]
+def laughlin_q1(nspins, flux, cf_flux: int = 1) -> float:
+    """Composite-fermion monopole strength Q1 = flux/2 - p (N - 1) (laughlin.py:34)."""
+    return float(flux) / 2 - int(cf_flux) * (sum(nspins) - 1)
+
+
+class LaughlinQuasiparticle:
+    """laughlin.py:19-100 for N = 2 Q1 + 2: log psi of walkers x [N, 2] (per walker, the
+    reference's f convention) or data [B, N, 2] (batched), complex128.  No parameters."""
+
+    def __init__(self, nspins, flux, cf_flux: int = 1, excitation_lz: float = 0.0, system=None):
+        self.nspins = tuple(int(n) for n in nspins)
+        self.flux = int(flux)
+        self.cf_flux = int(cf_flux)
+        self.excitation_lz = float(excitation_lz)
+        self.system = system
+        N = sum(self.nspins)
+        self.Q1 = laughlin_q1(self.nspins, self.flux, self.cf_flux)
+        if N != 2 * self.Q1 + 2:
+            raise ValueError(f"not a quasiparticle filling: N = {N}, Q1 = {self.Q1}")
+        diff = self.excitation_lz - self.Q1  # laughlin.py:49-52
+        if int(diff) != diff or not (-abs(self.Q1) - 1 <= self.excitation_lz <= abs(self.Q1) + 1):
+            raise ValueError(f"impossible Lz = {self.excitation_lz} for the quasiparticle (Q1 = {self.Q1})")
+
+    def init(self, key=None, data=None, device=None) -> dict:
+        return {}
+
+    def _logpsi(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.to(torch.float64)
+        N, Q, m1 = x.shape[0], self.Q1, self.excitation_lz
+        theta, phi = x[:, 0], x[:, 1]
+        u = (torch.cos(theta / 2) * torch.exp(0.5j * phi))[:, None]  # laughlin.py:61-62
+        v = (torch.sin(theta / 2) * torch.exp(-0.5j * phi))[:, None]
+        k = torch.arange(0, int(round(2 * Q)) + 1, device=x.device, dtype=torch.float64)  # Q + m, m = -Q .. Q
+        orbitals = u**k * v ** (2 * Q - k)
+        eye = torch.eye(N, dtype=u.dtype, device=x.device)
+        element = u * v[:, 0] - u[:, 0] * v + eye  # laughlin.py:91
+        jastrow = torch.prod(element, dim=-1, keepdim=True)
+        # LLL projection (u* -> d/du, v* -> d/dv), laughlin.py:93-95
+        jastrow_dv = jastrow * (torch.sum(-u[:, 0] / element, dim=-1, keepdim=True) + u)
+        jastrow_du = jastrow * (torch.sum(v[:, 0] / element, dim=-1, keepdim=True) - v)
+        excited = (u ** (Q + m1) * v ** (Q - m1)) * ((Q + 1 + m1) * v * jastrow_dv - (Q + 1 - m1) * u * jastrow_du)
+        orb = torch.cat([orbitals * jastrow, excited], dim=-1)
+        sign, logdet = torch.linalg.slogdet(orb)  # one determinant: log-sum-exp reduces to this
+        return logdet + torch.log(sign)
+
+    def __call__(self, params, data: torch.Tensor) -> torch.Tensor:
+        if data.dim() == 2:
+            return self._logpsi(data)
+        return torch.vmap(self._logpsi)(data)
+
+    apply = __call__
+
+
+__all__ = ["Laughlin", "LaughlinQuasiparticle", "laughlin_q1", "_lib", "_ptr", "_stream"]

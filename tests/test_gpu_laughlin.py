@@ -5,7 +5,8 @@
   Hessian through hamiltonian.py's formulas); the kernels work in double, so 1e-5.
 * Analytic pins on every walker of a full batch: the Laughlin ground state lies in the
   lowest Landau level with L = 0 (KE = N/2, L^2 = Lz = 0); the quasihole has L = Q1
-  (L^2 = Q1 (Q1 + 1), Lz = excitation_lz).
+  (L^2 = Q1 (Q1 + 1), Lz = excitation_lz); the quasiparticle (laughlin.py:82-100, through
+  the callable boundary) has L = Q1 + 1 = N/2.
 * The reference's CLI test restated (tests/cli_test.py:24-42): Laughlin N=3, 2Q=6,
   Coulomb, optimizer none, 100 iterations, seed 42, batch 3360 -> the energy log shows
   2.58 and L_square=0.0000.
@@ -77,13 +78,52 @@ def test_laughlin_analytic_pins(cuda, case, L2):
         assert np.max(err) < 1e-6, (k, np.max(err))
 
 
-def test_quasiparticle_is_rejected(cuda):
-    system = config.System(nspins=(4, 0), flux=8)
+@pytest.mark.parametrize("N,lz", [(4, 0.0), (4, 1.0), (4, -2.0), (6, 1.0)])
+def test_quasiparticle_analytic_pins(cuda, N, lz):
+    """laughlin.py:82-100 (N = 2 Q1 + 2, 2Q = 3 (N - 1) - 1): the LLL-projected quasiparticle
+    is a lowest-Landau-level state (KE = N/2 on every walker) with L = Q1 + 1 = N/2 and
+    Lz = excitation_lz, evaluated through the callable boundary (torch.func derivatives of
+    the reference's slogdet form, KE / Lz / L^2 assembled by dh_kinetic_from_derivatives)."""
+    from deephall_amd.networks import LaughlinQuasiparticle
+
+    flux = 3 * (N - 1) - 1
+    system = config.System(nspins=(N, 0), flux=flux, lz_center=lz)
     net = config.Network()
     net.type = config.NetworkType.laughlin
     model = make_network(system, net)
-    with pytest.raises(RuntimeError, match="quasiparticle"):
-        model.apply({}, torch.zeros(2, 4, 2, device=cuda))
+    assert isinstance(model, LaughlinQuasiparticle) and model.Q1 == (N - 2) / 2
+    x = torch.tensor(make_walkers(256, N, seed=5, margin=0.05), device=cuda)
+    e, o = hamiltonian.local_energy(model, system)(model.init(), x)
+    L = N / 2
+    st = torch.sin(x[..., 0].double().cpu())
+    geo = ((flux / 2) ** 2 * (1 / st).sum(-1) ** 2).numpy()  # size of the cancelling magnetic terms
+    for k, want in (("kinetic", N / 2), ("angular_momentum_square", L * (L + 1)), ("angular_momentum_z", lz),
+                    ("angular_momentum_z_square", lz * lz)):
+        err = np.abs(o[k].real.cpu().numpy() - want) / np.maximum(1.0, geo)
+        assert np.max(err) < 1e-5, (k, np.max(err))
+    assert np.max(np.abs(o["kinetic"].imag.cpu().numpy()) / np.maximum(1.0, geo)) < 1e-5
+
+
+def test_quasiparticle_mcmc(cuda):
+    """make_mcmc_step on the quasiparticle callable (the generic path: HIP proposal / accept on
+    the dh_mcmc_step random streams): walkers stay on the sphere, the acceptance is sane, and
+    log psi of the moved walkers equals the callable's."""
+    from deephall_amd.mcmc import make_mcmc_step
+    from deephall_amd.random import PRNGKey
+
+    system = config.System(nspins=(4, 0), flux=8, lz_center=1.0)
+    net = config.Network()
+    net.type = config.NetworkType.laughlin
+    model = make_network(system, net)
+    x = torch.tensor(make_walkers(512, 4, seed=9, margin=0.05), device=cuda).contiguous()
+    step = make_mcmc_step(model, batch_per_device=512, steps=5)
+    x, pmove = step(model.init(), x, PRNGKey(2), 0.3)
+    pm = float(pmove)
+    assert 0.05 < pm <= 1.0, pm
+    assert torch.isfinite(x).all()
+    assert (x[..., 0] >= 0).all() and (x[..., 0] <= np.pi).all()
+    lp = model(None, x)
+    assert torch.isfinite(lp.real).all()
 
 
 def test_cli_laughlin_energy(cuda, tmp_path):
