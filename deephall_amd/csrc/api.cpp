@@ -1053,7 +1053,8 @@ int dh_adam_update(float* params, const float* grad, float* mu, float* nu, size_
 
 int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int32_t* n_accept, int B, int steps,
                     int penalties, float* out, void* stream) {
-  if (!h || !e_l || !obs || !out) return fail(DH_EINVAL, "null argument");
+  (void)h;  // statistics of any wavefunction's E_L (NULL: a log-psi callable of the caller)
+  if (!e_l || !obs || !out) return fail(DH_EINVAL, "null argument");
   if (B < 1) return fail(DH_EINVAL, "dh_energy_stats needs B >= 1");
   launch_stats(e_l, obs, n_accept, B, steps, penalties, out, (hipStream_t)stream);
   return check_launch();
@@ -1061,7 +1062,8 @@ int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int3
 
 int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const float* stats, float lz_penalty,
                  float lz_center, float l2_penalty, float* diff, float* nvalid, void* stream) {
-  if (!h || !e_l || !obs || !stats || !diff || !nvalid) return fail(DH_EINVAL, "null argument");
+  (void)h;  // as dh_energy_stats: h may be NULL
+  if (!e_l || !obs || !stats || !diff || !nvalid) return fail(DH_EINVAL, "null argument");
   if (B < 1) return fail(DH_EINVAL, "dh_loss_diff needs B >= 1");
   launch_loss_diff(e_l, obs, B, stats, lz_penalty, lz_center, l2_penalty, diff, nvalid, (hipStream_t)stream);
   return check_launch();

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib, constants
 from .hamiltonian import _run_local_energy
-from .mcmc import resolve_network
+from .mcmc import native_network, resolve_network
 from .networks.psiformer import _ptr, _stream, get_handle
 
 # packed all-reduce: every DH_STAT_* entry (16 floats; the clipped Lz^2 / Lz / L^2 means
@@ -31,14 +31,19 @@ class LossMode(enum.Enum):
     SR_F_VECTOR = enum.auto()
 
 
+def _handle(net, device):
+    """The library handle of a native network, or NULL for a caller's log-psi callable."""
+    spec = getattr(net, "spec", None) if net is not None else None
+    return get_handle(spec, device).h if spec is not None else None
+
+
 def device_stats(net, e_l, obs, n_accept=None, steps=1, penalties=False):
     """dh_energy_stats on this rank: float32 [16] device tensor (DH_STAT_* layout)."""
-    h = get_handle(net.spec, e_l.device)
     out = torch.empty(_lib.DH_NSTATS, dtype=torch.float32, device=e_l.device)
     _lib.check(
-        h.lib.dh_energy_stats(
-            h.h, _ptr(e_l), _ptr(obs), _ptr(n_accept), e_l.shape[0], int(steps), int(bool(penalties)), _ptr(out),
-            _stream(e_l.device),
+        _lib.load().dh_energy_stats(
+            _handle(net, e_l.device), _ptr(e_l), _ptr(obs), _ptr(n_accept), e_l.shape[0], int(steps),
+            int(bool(penalties)), _ptr(out), _stream(e_l.device),
         )
     )
     return out
@@ -67,13 +72,12 @@ def loss_diff(net, e_l, obs, gstats, lz_penalty=0.0, lz_center=0.0, l2_penalty=0
     """dh_loss_diff: diff = iqr_clip(E_L - <E_L>_clip + penalties) (loss.py:75-89) with the
     reduced clipped means ``gstats`` (device, DH_STAT_* layout).  Returns (diff [B,2] f32,
     nvalid [1] f32 = walkers with a non-NaN diff)."""
-    h = get_handle(net.spec, e_l.device)
     B = e_l.shape[0]
     diff = torch.empty(B, 2, dtype=torch.float32, device=e_l.device)
     nvalid = torch.empty(1, dtype=torch.float32, device=e_l.device)
     _lib.check(
-        h.lib.dh_loss_diff(
-            h.h, _ptr(e_l), _ptr(obs), B, _ptr(gstats), float(lz_penalty), float(lz_center), float(l2_penalty),
+        _lib.load().dh_loss_diff(
+            _handle(net, e_l.device), _ptr(e_l), _ptr(obs), B, _ptr(gstats), float(lz_penalty), float(lz_center), float(l2_penalty),
             _ptr(diff), _ptr(nvalid), _stream(e_l.device),
         )
     )
@@ -95,9 +99,11 @@ def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_GRAD):
     or the complex one ({name: complex tensor}, SR_F_VECTOR).  Every statistic and the
     gradient are averaged over ranks: one packed all-reduce of the statistics, one of the
     gradient (the reference's Adam path skips the latter, SURVEY.md finding 9)."""
-    net = resolve_network(network)
     pen = (float(system.lz_penalty), float(system.lz_center), float(system.l2_penalty))
     penalties = pen[0] != 0.0 or pen[2] != 0.0
+    if native_network(network) is None:
+        return _make_callable_loss_fn(network, system, mode, pen, penalties)
+    net = resolve_network(network)
 
     def loss_and_grad(params, data, n_accept=None, steps=1):
         e_l, obs = _run_local_energy(net, params, data)
@@ -116,4 +122,36 @@ def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_GRAD):
         return stats, {k: torch.complex(grad[k], gim[k]) for k in grad}
 
     loss_and_grad.network = net
+    return loss_and_grad
+
+
+def _make_callable_loss_fn(f, system, mode, pen, penalties):
+    """make_loss_fn for a log-psi callable that is not a network of this library (e.g. the
+    Laughlin quasiparticle): E_L through deephall_amd.generic, then the same device statistics,
+    packed all-reduce and clipped difference.  Such a callable has no parameters here, so
+    only ENERGY_DIFF (optimizer none) is served."""
+    from . import generic
+
+    if mode != LossMode.ENERGY_DIFF:
+        raise TypeError("parameter gradients need a network of this library (Psiformer)")
+    e_fn = generic.local_energy(f, system)
+
+    def loss_and_grad(params, data, n_accept=None, steps=1):
+        e, o = e_fn(params, data)
+        B = e.shape[0]
+        e_l = torch.view_as_real(e.to(torch.complex64)).contiguous()
+        obs = torch.zeros(B, 8, dtype=torch.float32, device=e.device)  # KE re, im, PE, Lz, Lz^2, L^2
+        obs[:, 0] = o["kinetic"].real.float()
+        obs[:, 1] = o["kinetic"].imag.float()
+        obs[:, 2] = o["potential"].float()
+        obs[:, 3] = o["angular_momentum_z"].float()
+        obs[:, 4] = o["angular_momentum_z_square"].float()
+        obs[:, 5] = o["angular_momentum_square"].float()
+        local = device_stats(None, e_l, obs, n_accept, steps, penalties=penalties)
+        stats, g = reduce_stats(local, raw=True)
+        loss_and_grad.last = (e_l, obs)
+        diff, _ = loss_diff(None, e_l, obs, g, *pen)
+        return stats, torch.complex(diff[:, 0], diff[:, 1])
+
+    loss_and_grad.network = None
     return loss_and_grad

@@ -215,6 +215,7 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
 #define DH_STAT_CLIPPED_LZ2 13 /* nanmean iqr_clip(Lz^2)  (penalties) */
 #define DH_STAT_CLIPPED_LZ 14  /* nanmean iqr_clip(Lz)    (penalties) */
 #define DH_STAT_CLIPPED_L2 15  /* nanmean iqr_clip(L^2)   (penalties) */
+/* h may be NULL (E_L of a log-psi callable evaluated outside the library). */
 int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int32_t* n_accept, int B, int steps,
                     int penalties, float* out, void* stream);
 
@@ -223,7 +224,7 @@ int dh_energy_stats(dh_handle* h, const float* e_l, const float* obs, const int3
  *         + l2_penalty (L^2 - <L^2>_clip),    diff = iqr_clip(d)  (local quantiles)
  * with the <.>_clip means read from `stats` (device, DH_STAT_* layout, already averaged
  * over devices).  diff[B][2] (re, im; NaN where E_L is NaN); nvalid[1] = number of
- * walkers with a non-NaN diff (the nanmean count of loss.py:64). */
+ * walkers with a non-NaN diff (the nanmean count of loss.py:64).  h may be NULL. */
 int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const float* stats, float lz_penalty,
                  float lz_center, float l2_penalty, float* diff, float* nvalid, void* stream);
 

@@ -155,3 +155,26 @@ def test_cli_laughlin_energy(cuda, tmp_path):
     text = "\n".join(lines)
     assert "energy=2.58" in text
     assert all(r["L_square"] in ("0.0000", "-0.0000") for r in rows)
+
+
+def test_quasiparticle_train_inference(cuda, tmp_path):
+    """The deephall CLI flow (train.py:80-167, optimizer none) on the quasiparticle: MCMC and
+    statistics through the callable boundary; the logged L_square is L (L + 1) = 6 and Lz the
+    excitation_lz on every iteration (exact eigenstate), the kinetic energy N/2 = 2."""
+    cfg = Config.from_dict({
+        "seed": 7,
+        "batch_size": 256,
+        "system": {"nspins": (4, 0), "flux": 8, "lz_center": 1.0},
+        "network": {"type": "laughlin"},
+        "mcmc": {"burn_in": 5},
+        "optim": {"iterations": 4, "optimizer": "none"},
+        "log": {"save_path": str(tmp_path)},
+    })
+    train(cfg)
+    with open(tmp_path / "train_stats.csv") as f:
+        rows = list(csv.DictReader(f))
+    assert len(rows) == 4
+    for r in rows:
+        assert abs(float(r["L_square"]) - 6.0) < 1e-3, r
+        assert abs(float(r["Lz"]) - 1.0) < 1e-3, r
+        assert np.isfinite(float(r["energy"]))
