@@ -24,6 +24,14 @@ namespace dh {
 namespace {
 
 __device__ inline float ipow(float b, int e) { return e < 0 ? 0.f : (e == 0 ? 1.f : powf(b, (float)e)); }
+// integer power by squaring (det_value's envelope values: a few multiplies per power instead
+// of powf's log / exp; the same value to f32 rounding)
+__device__ inline float ipow_sq(float b, int e) {
+  float r = 1.f;
+  for (; e > 0; e >>= 1, b *= b)
+    if (e & 1) r *= b;
+  return r;
+}
 
 // F element (complex) of row `row` at (blk, m, j, k)
 struct FView {
@@ -45,14 +53,15 @@ struct EnvLeaf {
 // (north patch sigma = +1, south patch sigma = -1; 0 = reference gauge).  The network
 // channels then stay regular near the poles; the removed term i Q sum sigma phi is
 // added back analytically (in double) by the energy assembly.
-__device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves, float gauge = 0.f) {
+__device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves, float gauge = 0.f,
+                                   bool sq = false) {
   const int a = p, b = M - 1 - p;
   const float m = 0.5f * (float)(a - b) - gauge;
   float c, s;
   sincosf(0.5f * th, &s, &c);
   float sph, cph;
   sincosf(m * ph, &sph, &cph);
-  const float R = ipow(c, a) * ipow(s, b);
+  const float R = sq ? ipow_sq(c, a) * ipow_sq(s, b) : ipow(c, a) * ipow(s, b);
   EnvLeaf L;
   L.e0 = cf{norm * R * cph, norm * R * sph};
   if (leaves) {
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
   double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] unit vectors (double: close pairs)
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
-    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
+    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false, 0.f, true).e0;
   }
   for (int i = tid; i < N; i += nt) {
     double st, ct, sp, cp;
