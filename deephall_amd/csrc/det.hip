@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
   const int MNK = M * N * K;
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
-    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false).e0;
+    E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false, 0.f, true).e0;  // as det_value (powers by squaring)
   }
   for (int i = tid; i < N; i += nt) {
     double st, ct_, sp, cp;
