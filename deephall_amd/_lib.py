@@ -70,6 +70,10 @@ EXPORTS = [
     "dh_profile_enable",
     "dh_profile_read",
     "dh_debug_f_offset",
+    "dh_kfac_layout",
+    "dh_kfac_workspace_bytes",
+    "dh_kfac_vjp",
+    "dh_kfac_step",
 ]
 
 
@@ -79,6 +83,7 @@ PROF_KINDS = ["gemm", "attention", "layernorm", "input", "det_value", "det_energ
 
 class DhConfig(C.Structure):
     _fields_ = [
+        ("struct_size", C.c_uint32),
         ("n_up", C.c_int),
         ("n_dn", C.c_int),
         ("flux", C.c_int),
@@ -94,6 +99,10 @@ class DhConfig(C.Structure):
         ("excitation_lz", C.c_float),
         ("cf_flux", C.c_int),
     ]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        self.struct_size = C.sizeof(DhConfig)
 
 
 _lib = None
@@ -171,6 +180,14 @@ def load(path: Path | str | None = None):
     lib.dh_vjp_workspace_bytes.restype = sz
     lib.dh_logpsi_vjp.argtypes = [vp, vp, i32, vp, vp, vp, vp, sz, vp]
     lib.dh_logpsi_vjp.restype = i32
+    lib.dh_kfac_layout.argtypes = [vp, C.POINTER(sz), i32]
+    lib.dh_kfac_layout.restype = i32
+    lib.dh_kfac_workspace_bytes.argtypes = [vp, i32]
+    lib.dh_kfac_workspace_bytes.restype = sz
+    lib.dh_kfac_vjp.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]
+    lib.dh_kfac_vjp.restype = i32
+    lib.dh_kfac_step.argtypes = [vp, vp, vp, f32, f32, vp, vp, f32, f32, f32, vp, vp, vp, sz, vp]
+    lib.dh_kfac_step.restype = i32
     lib.dh_grad_cotangent.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.dh_grad_cotangent.restype = i32
     lib.dh_adam_update.argtypes = [vp, vp, vp, vp, sz, f32, f32, f32, f32, i32, vp]

@@ -114,8 +114,8 @@ class OptimizerKfac:
 
 @dataclass
 class Optim:
-    """config.py:160-165.  The reference's default optimizer is KFAC, which is not built
-    on MI355X (optimizers.py raises for it); Adam and 'none' are."""
+    """config.py:160-165.  The default optimizer is KFAC, as in the reference
+    (optimizers.py: make_kfac_training_step on the dh_kfac_* kernels)."""
 
     iterations: int = 1000
     optimizer: Optional[OptimizerName] = OptimizerName.kfac

@@ -90,6 +90,31 @@ struct Profiler {
   size_t used = 0;
 };
 
+// KFAC plan (dh_kfac_*): factor slots of the statistics buffer, the dense blocks and the
+// generic parameters (oracle/kfac.py restates the algorithm), plus device job tables.
+struct KfacLayerSlots {
+  int A_h, G_q, G_k, G_v, A_o, G_T, A_Wl, G_out, A_h1, G_z;
+};
+struct KfacHost {
+  std::vector<KfacSlot> slots;
+  size_t nmat = 0;     // floats of all factor slots
+  size_t nstats = 0;   // + the generic diagonal
+  int s_feat = -1, s_h0 = -1;
+  KfacLayerSlots lay[16];
+  int A_orb[2] = {-1, -1}, G_orb[2][2] = {{-1, -1}, {-1, -1}};
+  struct Blk {
+    int kseg, bseg, din, dout, a, g;
+    float scale;
+  };
+  std::vector<Blk> blocks;
+  std::vector<KfacInvJob> inv;
+  std::vector<KfacBlockJob> bjobs;
+  std::vector<KfacGemmJob> g1, g2;
+  size_t kbuf_doubles = 0;  // inverse matrices + V, T, P V per block
+  KfacDevPlan dev{};
+  void* dev_mem = nullptr;  // one allocation for the device tables
+};
+
 struct dh_handle {
   dh_config cfg;
   Dims d;
@@ -110,6 +135,7 @@ struct dh_handle {
   bool laughlin = false;          // DH_NETWORK_LAUGHLIN: no parameters, laughlin.hip kernels
   std::vector<int> expo_host;     // Laughlin exponents [2][N] = (Q1 + m_j, Q1 - m_j)
   int* expo = nullptr;            // device copy (uploaded at first use)
+  KfacHost* kfac = nullptr;       // KFAC plan (built at first dh_kfac_* call)
   Profiler prof;
 };
 
@@ -180,6 +206,9 @@ int laughlin_exponents(const dh_config* cfg, std::vector<int>& ex) {
 
 int dh_create(const dh_config* cfg, dh_handle** out) {
   if (!cfg || !out) return fail(DH_EINVAL, "null argument");
+  if (cfg->struct_size != sizeof(dh_config))
+    return fail(DH_EINVAL, "dh_config.struct_size must equal sizeof(dh_config) (" + std::to_string(sizeof(dh_config)) +
+                               " bytes); the caller's binding has a different layout");
   if (cfg->network_type == DH_NETWORK_LAUGHLIN) {
     const int N = cfg->n_up + cfg->n_dn;
     if (cfg->n_up < 0 || cfg->n_dn < 0 || N < 1 || N > 32) return fail(DH_EINVAL, "need 1 <= N <= 32 electrons");
@@ -330,6 +359,10 @@ void dh_destroy(dh_handle* h) {
   if (h->wb) (void)hipFree(h->wb);
   if (h->wbt) (void)hipFree(h->wbt);
   if (h->expo) (void)hipFree(h->expo);
+  if (h->kfac) {
+    if (h->kfac->dev_mem) (void)hipFree(h->kfac->dev_mem);
+    delete h->kfac;
+  }
   delete h;
 }
 
@@ -830,10 +863,11 @@ struct GradWork {
   float *dh, *dA, *dz, *dqkv, *dO;                            // backward temporaries
   float *P, *dWol, *dbol;                                     // chunk partials, folded-weight grads
   float *dWorb, *dborb;                                       // full-layout orbital grads ("sparse")
+  float *fgrad, *ctf;                                         // KFAC: Fisher tangent (ref layout), cotangent
   size_t total_bytes;
 };
 
-GradWork carve_grad(const Dims& d, int nw, void* base) {
+GradWork carve_grad(const Dims& d, int nw, void* base, size_t nref = 0) {
   const int rows = nw * d.N;
   const size_t rp = (size_t)round_up(std::max(rows, 1), kRowPad);
   const size_t D = d.D, nh = align64(rp * D);
@@ -863,7 +897,9 @@ GradWork carve_grad(const Dims& d, int nw, void* base) {
   w.dqkv = take(3 * nh);
   w.dO = take(nh);
   const size_t nch = (size_t)grad_chunks(rows);
-  const size_t pw = std::max({D * 3 * D, D * (size_t)d.ld_orb, (size_t)4 * D});
+  const size_t MNK = (size_t)d.M * d.N * d.K;
+  // (KFAC: the orbital output Gram matrices need MNK^2 per chunk)
+  const size_t pw = std::max({D * 3 * D, D * (size_t)d.ld_orb, (size_t)4 * D, nref ? MNK * MNK : (size_t)0});
   const size_t pc = std::max((size_t)3 * D, (size_t)d.ld_orb);
   w.P = take(std::max({nch * pw, nch * pc, (size_t)ln_bwd_blocks(rows) * 2 * D, (size_t)nw * 2}));
   w.dWol = take(D * D);
@@ -872,23 +908,30 @@ GradWork carve_grad(const Dims& d, int nw, void* base) {
     w.dWorb = take(D * d.ld_orb);
     w.dborb = take(d.ld_orb);
   }
+  if (nref) {
+    w.fgrad = take(nref);
+    w.ctf = take((size_t)nw * 2);
+  }
   w.total_bytes = off * sizeof(float);
   return w;
 }
 
-// One chunk of the VJP: forward with saved activations, then the chain rule back to every
-// reference parameter; gradient written (acc = 0) or accumulated (acc = 1) into `grad`
-// (dh_ref_layout).  ct: per-walker cotangents [nw][2].
-int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, float* logpsi, int acc,
-            const GradWork& w, hipStream_t s) {
+// KFAC statistics accumulated by a Fisher-mode backward pass (vjp_backward with kf != null):
+// factor Gram matrices into `stats` (KfacHost slots), normalised by the total row counts.
+struct KfacAcc {
+  const KfacHost* plan;
+  float* stats;
+  float inv_rows;         // 1 / (B N)
+  float inv_rows_blk[2];  // 1 / (B N_alpha) (orbital blocks)
+  int acc;                // accumulate into stats (chunks after the first)
+};
+
+// forward with saved activations (the same arithmetic as the log-psi pass)
+void vjp_forward(dh_handle* h, const float* x, int nw, float* logpsi, const GradWork& w, hipStream_t s) {
   const Dims& d = h->d;
   const Params& P = h->p;
-  const int rows = nw * d.N, D = d.D, nch = grad_chunks(rows);
+  const int rows = nw * d.N, D = d.D;
   const bool x6 = d.D % 32 == 0 && gemm_x6_supported(D);
-  const RefSeg RS{d.L, d.NB, d.sparse};
-  auto g = [&](int seg) { return grad + h->ref_offsets[seg]; };
-  auto ref = [&](int seg) { return (const float*)h->ref + h->ref_offsets[seg]; };
-  // forward GEMM Y = X W (+ bias) (+ R): the same arithmetic as the log-psi pass
   auto fwd = [&](const float* X, const float* W, const float* Wt, const uint16_t* Wp, int ncols, const float* bias,
                  const float* Rr, float* Y) {
     if (x6)
@@ -898,23 +941,6 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
     else
       launch_gemm(X, D, W, ncols, bias, Rr, ncols, Y, ncols, rows, ncols, D, 1, s);
   };
-  // backward GEMM dX = dY W^T (+ R) with W [D][n]
-  auto bwd = [&](const float* dY, int n, const uint16_t* WB, const float* WBT, const float* Rr, float* dX) {
-    if (x6)
-      launch_gemm_x6(dY, n, WB, x6_plane_rows(D), nullptr, Rr, D, dX, D, rows, D, n, 1, s);
-    else
-      launch_gemm(dY, n, WBT, D, nullptr, Rr, D, dX, D, rows, D, n, 1, s);
-  };
-  // weight gradient: out[:, c0:c0+nc] (ldo) (+)= X^T dY[:, c0:c0+nc] over this chunk's rows
-  auto wgrad = [&](const float* X, const float* dY, int n) { launch_tn_partial(X, D, dY, n, rows, D, n, w.P, s); };
-  auto wout = [&](int n, int c0, int nc, float* out, int ldo) {
-    launch_reduce2d(w.P + c0, nch, (size_t)D * n, n, D, nc, out, ldo, 1.f, acc, s);
-  };
-  auto bgrad = [&](const float* dY, int n, int c0, int nc, float* out) {
-    launch_colsum_partial(dY, n, rows, n, w.P, s);
-    launch_reduce2d(w.P + c0, nch, (size_t)n, n, 1, nc, out, nc, 1.f, acc, s);
-  };
-  // ---- forward with saved activations
   launch_input(d, x, P.W0, nullptr, nullptr, w.hs[0], nullptr, w.geo, nw, 1, s);
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
@@ -936,32 +962,100 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
       launch_gemm(hL, D, P.Worb, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, rows, d.orb_cols, D, 1, s);
   }
   launch_det_value(d, w.F, x, P.jastrow, h->norm, logpsi ? logpsi : w.logpsi, nw, s);
+}
+
+// Reverse pass over the saved activations of vjp_forward: the parameter gradient for the
+// per-walker cotangents ct, written (acc = 0) or accumulated (acc = 1) into `grad`
+// (dh_ref_layout).  Fisher mode (kf != null): the dense weight gradients are skipped (only
+// the LayerNorm and Jastrow entries of `grad` are written — KFAC's generic tangents) and
+// every dense layer's input / output-tangent Gram matrices go into kf->stats.
+int vjp_backward(dh_handle* h, const float* x, int nw, const float* ct, float* grad, int acc, const GradWork& w,
+                 hipStream_t s, const KfacAcc* kf = nullptr) {
+  const Dims& d = h->d;
+  const Params& P = h->p;
+  const int rows = nw * d.N, D = d.D, nch = grad_chunks(rows);
+  const bool x6 = d.D % 32 == 0 && gemm_x6_supported(D);
+  const RefSeg RS{d.L, d.NB, d.sparse};
+  const bool fisher = kf != nullptr;
+  auto g = [&](int seg) { return grad + h->ref_offsets[seg]; };
+  auto ref = [&](int seg) { return (const float*)h->ref + h->ref_offsets[seg]; };
+  // backward GEMM dX = dY W^T (+ R) with W [D][n]
+  auto bwd = [&](const float* dY, int n, const uint16_t* WB, const float* WBT, const float* Rr, float* dX) {
+    if (x6)
+      launch_gemm_x6(dY, n, WB, x6_plane_rows(D), nullptr, Rr, D, dX, D, rows, D, n, 1, s);
+    else
+      launch_gemm(dY, n, WBT, D, nullptr, Rr, D, dX, D, rows, D, n, 1, s);
+  };
+  // weight gradient: out[:, c0:c0+nc] (ldo) (+)= X^T dY[:, c0:c0+nc] over this chunk's rows
+  auto wgrad = [&](const float* X, const float* dY, int n) { launch_tn_partial(X, D, dY, n, rows, D, n, w.P, s); };
+  auto wout = [&](int n, int c0, int nc, float* out, int ldo) {
+    launch_reduce2d(w.P + c0, nch, (size_t)D * n, n, D, nc, out, ldo, 1.f, acc, s);
+  };
+  auto bgrad = [&](const float* dY, int n, int c0, int nc, float* out) {
+    launch_colsum_partial(dY, n, rows, n, w.P, s);
+    launch_reduce2d(w.P + c0, nch, (size_t)n, n, 1, nc, out, nc, 1.f, acc, s);
+  };
+  // KFAC Gram matrices: slot (+)= scale X^T X (n columns of X, row stride ldx, `nr` rows),
+  // with the bias row / column / corner of [X, 1] when aug
+  auto gram = [&](const float* X, int ldx, int n, int slot, float scale, int nr, bool aug) {
+    const KfacSlot& sl = kf->plan->slots[slot];
+    float* out = kf->stats + sl.off;
+    const int nc2 = grad_chunks(nr);
+    launch_tn_partial(X, ldx, X, ldx, nr, n, n, w.P, s);
+    launch_reduce2d(w.P, nc2, (size_t)n * n, n, n, n, out, sl.n, scale, kf->acc, s);
+    if (aug) {
+      launch_colsum_partial(X, ldx, nr, n, w.P, s);
+      launch_kfac_aug(w.P, nc2, n, out, sl.n, scale, (float)nr * scale, kf->acc, s);
+    }
+  };
   // ---- backward
   launch_det_bwd(d, w.F, x, P.jastrow, h->norm, ct, w.dF, w.jg, nw, s);
   launch_reduce2d(w.jg, nw, 2, 2, 1, 1, g(RS.jas(0)), 1, 1.f, acc, s);
   launch_reduce2d(w.jg + 1, nw, 2, 2, 1, 1, g(RS.jas(1)), 1, 1.f, acc, s);
   {
     const int MNK = d.M * d.N * d.K;
-    wgrad(w.hs[d.L], w.dF, d.ld_orb);
-    if (!d.sparse) {
-      for (int i = 0; i < 2 * d.NB; ++i) wout(d.ld_orb, i * MNK, MNK, g(RS.orb_kernel(i)), MNK);
-      launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
-      for (int i = 0; i < 2 * d.NB; ++i)
-        launch_reduce2d(w.P + i * MNK, nch, (size_t)d.ld_orb, d.ld_orb, 1, MNK, g(RS.orb_bias(i)), MNK, 1.f, acc, s);
-    } else {
-      // full-layout gradients of this chunk, then through the lll_weight fold
-      launch_reduce2d(w.P, nch, (size_t)D * d.ld_orb, d.ld_orb, D, d.orb_cols, w.dWorb, d.ld_orb, 1.f, 0, s);
-      launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
-      launch_reduce2d(w.P, nch, (size_t)d.ld_orb, d.ld_orb, 1, d.orb_cols, w.dborb, d.ld_orb, 1.f, 0, s);
-      SparseBlocks sb{};
-      sb.n = 2 * d.NB;
-      for (int i = 0; i < sb.n; ++i) {
-        sb.W8[i] = ref(RS.orb_kernel(i));
-        sb.b8[i] = ref(RS.orb_bias(i));
-        launch_sparse_unfold(w.dWorb + i * MNK, d.ld_orb, w.dborb + i * MNK, ref(RS.lll(0)), D, d.N * d.K, d.M,
-                             g(RS.orb_kernel(i)), g(RS.orb_bias(i)), acc, s);
+    if (fisher) {
+      const KfacHost& K = *kf->plan;
+      int lo = 0;
+      for (int a = 0, blk = 0; a < 2; ++a) {
+        const int na = a == 0 ? d.n_up : d.n_dn;
+        if (na == 0) continue;
+        for (int part = 0; part < 2; ++part)
+          gram(w.dF + (size_t)(blk * 2 + part) * MNK, d.ld_orb, MNK, K.G_orb[blk][part], kf->inv_rows_blk[blk], rows,
+               false);
+        if (d.NB == 1) {
+          gram(w.hs[d.L], D, D, K.A_orb[blk], kf->inv_rows_blk[blk], rows, true);
+        } else {  // this spin block's rows of every walker, gathered
+          launch_copy2d(w.hs[d.L] + (size_t)lo * D, d.N * D, w.dqkv, na * D, nw, na * D, s);
+          gram(w.dqkv, D, D, K.A_orb[blk], kf->inv_rows_blk[blk], nw * na, true);
+        }
+        lo += na;
+        ++blk;
       }
-      launch_sparse_lll_grad(sb, w.dWorb, d.ld_orb, w.dborb, D, d.N * d.K, d.M, g(RS.lll(0)), g(RS.lll(1)), acc, s);
+    } else {
+      wgrad(w.hs[d.L], w.dF, d.ld_orb);
+      if (!d.sparse) {
+        for (int i = 0; i < 2 * d.NB; ++i) wout(d.ld_orb, i * MNK, MNK, g(RS.orb_kernel(i)), MNK);
+        launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
+        for (int i = 0; i < 2 * d.NB; ++i)
+          launch_reduce2d(w.P + i * MNK, nch, (size_t)d.ld_orb, d.ld_orb, 1, MNK, g(RS.orb_bias(i)), MNK, 1.f, acc,
+                          s);
+      } else {
+        // full-layout gradients of this chunk, then through the lll_weight fold
+        launch_reduce2d(w.P, nch, (size_t)D * d.ld_orb, d.ld_orb, D, d.orb_cols, w.dWorb, d.ld_orb, 1.f, 0, s);
+        launch_colsum_partial(w.dF, d.ld_orb, rows, d.ld_orb, w.P, s);
+        launch_reduce2d(w.P, nch, (size_t)d.ld_orb, d.ld_orb, 1, d.orb_cols, w.dborb, d.ld_orb, 1.f, 0, s);
+        SparseBlocks sb{};
+        sb.n = 2 * d.NB;
+        for (int i = 0; i < sb.n; ++i) {
+          sb.W8[i] = ref(RS.orb_kernel(i));
+          sb.b8[i] = ref(RS.orb_bias(i));
+          launch_sparse_unfold(w.dWorb + i * MNK, d.ld_orb, w.dborb + i * MNK, ref(RS.lll(0)), D, d.N * d.K, d.M,
+                               g(RS.orb_kernel(i)), g(RS.orb_bias(i)), acc, s);
+        }
+        launch_sparse_lll_grad(sb, w.dWorb, d.ld_orb, w.dborb, D, d.N * d.K, d.M, g(RS.lll(0)), g(RS.lll(1)), acc,
+                               s);
+      }
     }
     bwd(w.dF, d.ld_orb, P.WorbB, P.WorbBT, nullptr, w.dh);
   }
@@ -973,39 +1067,227 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
     launch_reduce2d(w.P, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln2s)), D, 1.f, acc, s);
     launch_reduce2d(w.P + D, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln2b)), D, 1.f, acc, s);
     // z = h1 Wm + bm
-    wgrad(w.h1[l], w.dz, D);
-    wout(D, 0, D, g(RS.lay(l, RWm)), D);
-    bgrad(w.dz, D, 0, D, g(RS.lay(l, Rbm)));
+    if (fisher) {
+      gram(w.dz, D, D, kf->plan->lay[l].G_z, kf->inv_rows, rows, false);
+      gram(w.h1[l], D, D, kf->plan->lay[l].A_h1, kf->inv_rows, rows, true);
+    } else {
+      wgrad(w.h1[l], w.dz, D);
+      wout(D, 0, D, g(RS.lay(l, RWm)), D);
+      bgrad(w.dz, D, 0, D, g(RS.lay(l, Rbm)));
+    }
     bwd(w.dz, D, lp.WmB, lp.WmBT, w.dA, w.dh);  // dh1 = dU + dz Wm^T
     // h1 = LN1(t): dT -> dA
     launch_ln_bwd(w.t[l], nullptr, lp.ln1, w.dh, nullptr, w.dA, nullptr, w.P, rows, D, s);
     launch_reduce2d(w.P, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln1s)), D, 1.f, acc, s);
     launch_reduce2d(w.P + D, nb, (size_t)2 * D, D, 1, D, g(RS.lay(l, Rln1b)), D, 1.f, acc, s);
     // t = h + o Wol + bol: folded-weight gradients, then unfolded onto Wo, bo, Wl
-    wgrad(w.o[l], w.dA, D);
-    launch_reduce2d(w.P, nch, (size_t)D * D, D, D, D, w.dWol, D, 1.f, 0, s);
-    launch_colsum_partial(w.dA, D, rows, D, w.P, s);
-    launch_reduce2d(w.P, nch, (size_t)D, D, 1, D, w.dbol, D, 1.f, 0, s);
-    //   Wol = Wo Wl, bol = bo Wl:  dWo = dWol Wl^T, dbo = dbol Wl^T, dWl = Wo^T dWol + bo^T dbol
-    launch_small_gemm(D, D, D, w.dWol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, RWo)), D, acc, s);
-    launch_small_gemm(1, D, D, w.dbol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, Rbo)), D, acc, s);
-    launch_small_gemm(D, D, D, ref(RS.lay(l, RWo)), D, 1, w.dWol, D, 0, g(RS.lay(l, RWl)), D, acc, s);
-    launch_small_gemm(D, D, 1, ref(RS.lay(l, Rbo)), 1, 0, w.dbol, D, 0, g(RS.lay(l, RWl)), D, 1, s);
+    if (fisher) {
+      // Dense_{2l+1}'s output tangent is dT; the attention output's input is o
+      gram(w.dA, D, D, kf->plan->lay[l].G_T, kf->inv_rows, rows, false);
+      gram(w.o[l], D, D, kf->plan->lay[l].A_o, kf->inv_rows, rows, true);
+    } else {
+      wgrad(w.o[l], w.dA, D);
+      launch_reduce2d(w.P, nch, (size_t)D * D, D, D, D, w.dWol, D, 1.f, 0, s);
+      launch_colsum_partial(w.dA, D, rows, D, w.P, s);
+      launch_reduce2d(w.P, nch, (size_t)D, D, 1, D, w.dbol, D, 1.f, 0, s);
+      //   Wol = Wo Wl, bol = bo Wl:  dWo = dWol Wl^T, dbo = dbol Wl^T, dWl = Wo^T dWol + bo^T dbol
+      launch_small_gemm(D, D, D, w.dWol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, RWo)), D, acc, s);
+      launch_small_gemm(1, D, D, w.dbol, D, 0, ref(RS.lay(l, RWl)), D, 1, g(RS.lay(l, Rbo)), D, acc, s);
+      launch_small_gemm(D, D, D, ref(RS.lay(l, RWo)), D, 1, w.dWol, D, 0, g(RS.lay(l, RWl)), D, acc, s);
+      launch_small_gemm(D, D, 1, ref(RS.lay(l, Rbo)), 1, 0, w.dbol, D, 0, g(RS.lay(l, RWl)), D, 1, s);
+    }
     bwd(w.dA, D, lp.WolB, lp.WolBT, nullptr, w.dO);  // dO = dT Wol^T
     launch_attn_bwd(d, w.qkv[l], w.dO, w.dqkv, nw, s);
     // qkv = h Wqkv + bqkv
-    wgrad(w.hs[l], w.dqkv, 3 * D);
-    for (int part = 0; part < 3; ++part) wout(3 * D, part * D, D, g(RS.lay(l, RWq + 2 * part)), D);
-    launch_colsum_partial(w.dqkv, 3 * D, rows, 3 * D, w.P, s);
-    for (int part = 0; part < 3; ++part)
-      launch_reduce2d(w.P + part * D, nch, (size_t)3 * D, 3 * D, 1, D, g(RS.lay(l, Rbq + 2 * part)), D, 1.f, acc,
-                      s);
+    if (fisher) {
+      const KfacLayerSlots& ls = kf->plan->lay[l];
+      const int gs[3] = {ls.G_q, ls.G_k, ls.G_v};
+      for (int part = 0; part < 3; ++part) gram(w.dqkv + part * D, 3 * D, D, gs[part], kf->inv_rows, rows, false);
+      gram(w.hs[l], D, D, ls.A_h, kf->inv_rows, rows, true);
+    } else {
+      wgrad(w.hs[l], w.dqkv, 3 * D);
+      for (int part = 0; part < 3; ++part) wout(3 * D, part * D, D, g(RS.lay(l, RWq + 2 * part)), D);
+      launch_colsum_partial(w.dqkv, 3 * D, rows, 3 * D, w.P, s);
+      for (int part = 0; part < 3; ++part)
+        launch_reduce2d(w.P + part * D, nch, (size_t)3 * D, 3 * D, 1, D, g(RS.lay(l, Rbq + 2 * part)), D, 1.f, acc,
+                        s);
+    }
     bwd(w.dqkv, 3 * D, lp.WqkvB, lp.WqkvBT, w.dA, w.dh);  // dh_l = dT + dqkv Wqkv^T
   }
   // h_0 = features W0
-  launch_w0_partial(d, w.geo, w.dh, D, rows, w.P, s);
-  launch_reduce2d(w.P, nch, (size_t)4 * D, D, 4, D, g(RS.W0()), D, 1.f, acc, s);
+  if (fisher) {
+    gram(w.dh, D, D, kf->plan->s_h0, kf->inv_rows, rows, false);
+    const KfacSlot& sl = kf->plan->slots[kf->plan->s_feat];
+    launch_kfac_feat_gram(d, w.geo, rows, w.P, s);
+    launch_reduce2d(w.P, nch, 16, 4, 4, 4, kf->stats + sl.off, 4, kf->inv_rows, kf->acc, s);
+  } else {
+    launch_w0_partial(d, w.geo, w.dh, D, rows, w.P, s);
+    launch_reduce2d(w.P, nch, (size_t)4 * D, D, 4, D, g(RS.W0()), D, 1.f, acc, s);
+  }
   return check_launch();
+}
+
+// One chunk of the VJP: forward with saved activations, then the chain rule back to every
+// reference parameter; gradient written (acc = 0) or accumulated (acc = 1) into `grad`
+// (dh_ref_layout).  ct: per-walker cotangents [nw][2].
+int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, float* logpsi, int acc,
+            const GradWork& w, hipStream_t s) {
+  vjp_forward(h, x, nw, logpsi, w, s);
+  return vjp_backward(h, x, nw, ct, grad, acc, w, s);
+}
+
+
+// ---- KFAC (optimizers/kfac.py:195-241; oracle/kfac.py)
+
+// Build the factor slots, dense blocks, generic segments and device job tables.
+int kfac_plan(dh_handle* h) {
+  if (h->kfac) return DH_OK;
+  const Dims& d = h->d;
+  if (d.sparse) return fail(DH_EINVAL, "KFAC: sparse orbitals are not supported (use orbital 'full')");
+  if (d.L > 16) return fail(DH_EINVAL, "KFAC: too many layers");
+  auto* K = new KfacHost();
+  const int D = d.D, N = d.N, MNK = d.M * d.N * d.K;
+  auto slot = [&](int n) {
+    K->slots.push_back(KfacSlot{n, K->nmat});
+    K->nmat += align64((size_t)n * n);
+    return (int)K->slots.size() - 1;
+  };
+  const RefSeg RS{d.L, d.NB, d.sparse};
+  auto blk = [&](int kseg, int bseg, int din, int dout, int a, int g, float scale) {
+    K->blocks.push_back(KfacHost::Blk{kseg, bseg, din, dout, a, g, scale});
+  };
+  K->s_feat = slot(4);
+  K->s_h0 = slot(D);
+  blk(RS.W0(), -1, 4, D, K->s_feat, K->s_h0, (float)N);
+  for (int l = 0; l < d.L; ++l) {
+    KfacLayerSlots& L = K->lay[l];
+    L.A_h = slot(D + 1);
+    L.G_q = slot(D);
+    L.G_k = slot(D);
+    L.G_v = slot(D);
+    L.A_o = slot(D + 1);
+    L.G_out = slot(D);
+    L.A_Wl = slot(D);
+    L.G_T = slot(D);
+    L.A_h1 = slot(D + 1);
+    L.G_z = slot(D);
+    blk(RS.lay(l, RWq), RS.lay(l, Rbq), D, D, L.A_h, L.G_q, (float)N);
+    blk(RS.lay(l, RWk), RS.lay(l, Rbk), D, D, L.A_h, L.G_k, (float)N);
+    blk(RS.lay(l, RWv), RS.lay(l, Rbv), D, D, L.A_h, L.G_v, (float)N);
+    blk(RS.lay(l, RWo), RS.lay(l, Rbo), D, D, L.A_o, L.G_out, (float)(N * d.H));  // x [B, N, H, dh]
+    blk(RS.lay(l, RWl), -1, D, D, L.A_Wl, L.G_T, (float)N);
+    blk(RS.lay(l, RWm), RS.lay(l, Rbm), D, D, L.A_h1, L.G_z, (float)N);
+  }
+  for (int a = 0, b = 0; a < 2; ++a) {
+    const int na = a == 0 ? d.n_up : d.n_dn;
+    if (na == 0) continue;
+    K->A_orb[b] = slot(D + 1);
+    for (int part = 0; part < 2; ++part) {
+      K->G_orb[b][part] = slot(MNK);
+      blk(RS.orb_kernel(2 * b + part), RS.orb_bias(2 * b + part), D, MNK, K->A_orb[b], K->G_orb[b][part], (float)na);
+    }
+    ++b;
+  }
+  // generic (diagonal) parameters: LayerNorm scale / bias, Jastrow alphas
+  KfacGenTable& G = K->dev.gen;
+  G = KfacGenTable{};
+  auto gen = [&](int seg, int n) {
+    G.ref[G.n] = h->ref_offsets[seg];
+    G.cmp[G.n] = G.total;
+    G.total += n;
+    ++G.n;
+  };
+  for (int l = 0; l < d.L; ++l)
+    for (int k : {Rln1s, Rln1b, Rln2s, Rln2b}) gen(RS.lay(l, k), D);
+  gen(RS.jas(0), 1);
+  gen(RS.jas(1), 1);
+  K->nstats = K->nmat + (size_t)G.total;
+  // inverse jobs (2 per block: A side, G side), then V / T / P V per block, all in one f64 buffer
+  size_t off = 0;
+  int nmax = 0, max_v = 0, max_m = 0, max_n = 0;
+  for (const auto& b : K->blocks) {
+    for (int side = 0; side < 2; ++side) {
+      KfacInvJob j{};
+      j.slot = side == 0 ? b.a : b.g;
+      j.partner = side == 0 ? b.g : b.a;
+      j.is_a = side == 0;
+      j.n = K->slots[j.slot].n;
+      j.sqrt_scale = std::sqrt(b.scale);
+      j.gj_off = off;
+      off += (size_t)j.n * j.n;
+      nmax = std::max(nmax, j.n);
+      K->inv.push_back(j);
+    }
+  }
+  for (size_t i = 0; i < K->blocks.size(); ++i) {
+    const auto& b = K->blocks[i];
+    const int dA = b.din + (b.bseg >= 0 ? 1 : 0);
+    KfacBlockJob j{};
+    j.kernel_off = h->ref_offsets[b.kseg];
+    j.bias_off = b.bseg >= 0 ? (long long)h->ref_offsets[b.bseg] : -1;
+    j.din = b.din;
+    j.dout = b.dout;
+    const size_t nv = (size_t)dA * b.dout;
+    j.v_off = off;
+    j.t_off = off + nv;
+    j.pv_off = off + 2 * nv;
+    off += 3 * nv;
+    K->bjobs.push_back(j);
+    K->g1.push_back(KfacGemmJob{K->inv[2 * i].gj_off, j.v_off, j.t_off, dA, b.dout, dA});
+    K->g2.push_back(KfacGemmJob{j.t_off, K->inv[2 * i + 1].gj_off, j.pv_off, dA, b.dout, b.dout});
+    max_v = std::max(max_v, (int)nv);
+    max_m = std::max(max_m, dA);
+    max_n = std::max(max_n, b.dout);
+  }
+  K->kbuf_doubles = off;
+  K->dev.nslots = (int)K->slots.size();
+  K->dev.njobs = (int)K->inv.size();
+  K->dev.nblocks = (int)K->blocks.size();
+  K->dev.nmax = nmax;
+  K->dev.max_v = max_v;
+  K->dev.max_m = max_m;
+  K->dev.max_n = max_n;
+  h->kfac = K;
+  return DH_OK;
+}
+
+// Upload the job tables (once, at the first device call).
+int kfac_device(dh_handle* h) {
+  if (int rc = kfac_plan(h)) return rc;
+  KfacHost* K = h->kfac;
+  if (K->dev_mem) return DH_OK;
+  // device tables
+  const size_t b1 = K->slots.size() * sizeof(KfacSlot), b2 = K->inv.size() * sizeof(KfacInvJob),
+               b3 = K->bjobs.size() * sizeof(KfacBlockJob), b4 = K->g1.size() * sizeof(KfacGemmJob);
+  auto al = [](size_t n) { return (n + 255) / 256 * 256; };
+  char* mem = nullptr;
+  if (hipMalloc(&mem, al(b1) + al(b2) + al(b3) + 2 * al(b4)) != hipSuccess) {
+    return fail(DH_EHIP, "KFAC: device table allocation failed");
+  }
+  K->dev_mem = mem;
+  K->dev.slots = reinterpret_cast<KfacSlot*>(mem);
+  K->dev.inv_jobs = reinterpret_cast<KfacInvJob*>(mem + al(b1));
+  K->dev.block_jobs = reinterpret_cast<KfacBlockJob*>(mem + al(b1) + al(b2));
+  K->dev.gemm1 = reinterpret_cast<KfacGemmJob*>(mem + al(b1) + al(b2) + al(b3));
+  K->dev.gemm2 = reinterpret_cast<KfacGemmJob*>(mem + al(b1) + al(b2) + al(b3) + al(b4));
+  bool ok = hipMemcpy(K->dev.slots, K->slots.data(), b1, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(K->dev.inv_jobs, K->inv.data(), b2, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(K->dev.block_jobs, K->bjobs.data(), b3, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(K->dev.gemm1, K->g1.data(), b4, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(K->dev.gemm2, K->g2.data(), b4, hipMemcpyHostToDevice) == hipSuccess;
+  if (!ok) {
+    (void)hipFree(mem);
+    K->dev_mem = nullptr;
+    return fail(DH_EHIP, "KFAC: device table upload failed");
+  }
+  return DH_OK;
+}
+
+size_t kfac_step_ws(const KfacHost* K) {
+  // kbuf (inverses, V, T, P V) | traces | GJ panel temporaries, doubles
+  const size_t nd = align64(K->kbuf_doubles) + align64(K->slots.size()) +
+                    align64(kfac_gj_tmp_doubles(K->dev.njobs, K->dev.nmax));
+  return nd * sizeof(double);
 }
 
 }  // namespace
@@ -1036,6 +1318,107 @@ int dh_logpsi_vjp(dh_handle* h, const float* x, int B, const float* ct, float* g
       return rc;
   }
   return DH_OK;
+}
+
+int dh_kfac_layout(dh_handle* h, size_t* out, int n) {
+  if (!h || h->laughlin) return fail(DH_EINVAL, "KFAC needs a Psiformer handle");
+  if (int rc = kfac_plan(h)) return rc;
+  const KfacHost& K = *h->kfac;
+  // [0] statistics floats, [1] factor-matrix floats, [2] slots, [3] dense blocks, [4] generic
+  // floats, [5] dh_kfac_step workspace bytes, then per block (kernel seg, bias seg or -1 as
+  // SIZE_MAX, din, dout, A slot, G slot, scale x 1000), then per slot (n, offset)
+  std::vector<size_t> v = {K.nstats, K.nmat, K.slots.size(), K.blocks.size(), (size_t)K.dev.gen.total,
+                           kfac_step_ws(&K)};
+  for (const auto& b : K.blocks)
+    v.insert(v.end(), {(size_t)b.kseg, b.bseg >= 0 ? (size_t)b.bseg : SIZE_MAX, (size_t)b.din, (size_t)b.dout,
+                       (size_t)b.a, (size_t)b.g, (size_t)std::lround(b.scale * 1000.f)});
+  for (const auto& sl : K.slots) v.insert(v.end(), {(size_t)sl.n, sl.off});
+  if (out)
+    for (int i = 0; i < n && i < (int)v.size(); ++i) out[i] = v[i];
+  return (int)v.size();
+}
+
+size_t dh_kfac_workspace_bytes(const dh_handle* h, int batch) {
+  if (!h || batch < 1) return 0;
+  return carve_grad(h->d, batch, nullptr, h->ref_offsets.back()).total_bytes;
+}
+
+int dh_kfac_vjp(dh_handle* h, const float* x, int B, const float* ct, float* grad, float* stats, float* logpsi,
+                void* ws, size_t ws_bytes, void* stream) {
+  if (!h || h->laughlin) return fail(DH_EINVAL, "KFAC needs a Psiformer handle");
+  const size_t nref = h->ref_offsets.back();
+  const size_t need1 = dh_kfac_workspace_bytes(h, 1);
+  if (int rc = check_common(h, x, B, ws, ws_bytes, need1)) return rc;
+  if (!h->ref_set) return fail(DH_ESTATE, "KFAC needs parameters uploaded with dh_set_params_ref");
+  if (!stats) return fail(DH_EINVAL, "null statistics buffer");
+  if (ct && !grad) return fail(DH_EINVAL, "ct given without grad");
+  if (h->d.D > 1024 || h->d.dh > 1024) return fail(DH_EINVAL, "KFAC supports D <= 1024");
+  if (int rc = kfac_device(h)) return rc;
+  const KfacHost& K = *h->kfac;
+  const Dims& d = h->d;
+  int chunk = B;
+  while (chunk > 1 && carve_grad(d, chunk, nullptr, nref).total_bytes > ws_bytes) chunk = (chunk + 1) / 2;
+  hipStream_t s = (hipStream_t)stream;
+  KfacAcc kf{};
+  kf.plan = &K;
+  kf.stats = stats;
+  kf.inv_rows = 1.f / ((float)B * d.N);
+  for (int a = 0, b = 0; a < 2; ++a) {
+    const int na = a == 0 ? d.n_up : d.n_dn;
+    if (na) kf.inv_rows_blk[b++] = 1.f / ((float)B * na);
+  }
+  const GradWork w = carve_grad(d, chunk, ws, nref);  // one layout: fgrad accumulates over chunks
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nw = std::min(chunk, B - b0);
+    const float* xc = x + (size_t)b0 * d.N * 2;
+    float* lp = logpsi ? logpsi + 2 * (size_t)b0 : w.logpsi;
+    vjp_forward(h, xc, nw, lp, w, s);
+    if (ct)
+      if (int rc = vjp_backward(h, xc, nw, ct + 2 * (size_t)b0, grad, b0 > 0, w, s)) return rc;
+    launch_kfac_fisher_ct(lp, nw, w.ctf, s);
+    kf.acc = b0 > 0;
+    if (int rc = vjp_backward(h, xc, nw, w.ctf, w.fgrad, b0 > 0, w, s, &kf)) return rc;
+  }
+  // derived factors of the folded attention output (the kernels run Wol = Wo Wl as one map):
+  // Dense_{2l+1}'s input a = [o, 1] [Wo; bo]:  A_Wl = [Wo; bo]^T A_o [Wo; bo]
+  // the attention output's tangent dT Wl^T:    G_out = Wl G_T Wl^T
+  const RefSeg RS{d.L, d.NB, d.sparse};
+  const int D = d.D;
+  auto ref = [&](int seg) { return (const float*)h->ref + h->ref_offsets[seg]; };
+  float* Wt = w.P;                        // [D + 1][D]
+  float* T = w.P + (size_t)(D + 1) * D;   // [D + 1][D]
+  for (int l = 0; l < d.L; ++l) {
+    const KfacLayerSlots& L = K.lay[l];
+    launch_copy2d(ref(RS.lay(l, RWo)), D, Wt, D, D, D, s);
+    launch_copy2d(ref(RS.lay(l, Rbo)), D, Wt + (size_t)D * D, D, 1, D, s);
+    launch_small_gemm(D + 1, D, D + 1, stats + K.slots[L.A_o].off, D + 1, 0, Wt, D, 0, T, D, 0, s);
+    launch_small_gemm(D, D, D + 1, Wt, D, 1, T, D, 0, stats + K.slots[L.A_Wl].off, D, 0, s);
+    launch_small_gemm(D, D, D, ref(RS.lay(l, RWl)), D, 0, stats + K.slots[L.G_T].off, D, 0, T, D, 0, s);
+    launch_small_gemm(D, D, D, T, D, 0, ref(RS.lay(l, RWl)), D, 1, stats + K.slots[L.G_out].off, D, 0, s);
+  }
+  launch_kfac_generic(w.fgrad, K.dev.gen, stats + K.nmat, 1.f / (float)B, s);
+  return check_launch();
+}
+
+int dh_kfac_step(dh_handle* h, float* raw, const float* stats, float ema, float weight, const float* grad,
+                 float* params, float lr, float damping, float norm_constraint, float* pgrad, double* info, void* ws,
+                 size_t ws_bytes, void* stream) {
+  if (!h || h->laughlin) return fail(DH_EINVAL, "KFAC needs a Psiformer handle");
+  if (!raw || !grad || !pgrad || !info || !ws) return fail(DH_EINVAL, "null argument");
+  if (!(weight > 0.f) || !(damping > 0.f)) return fail(DH_EINVAL, "KFAC needs weight > 0 and damping > 0");
+  if (int rc = kfac_device(h)) return rc;
+  const KfacHost& K = *h->kfac;
+  const size_t nref = h->ref_offsets.back();
+  if (ws_bytes < kfac_step_ws(&K)) return fail(DH_ENOMEM, "KFAC step workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  double* kbuf = reinterpret_cast<double*>(ws);
+  double* tr = kbuf + align64(K.kbuf_doubles);
+  double* tmp = tr + align64(K.slots.size());
+  if (stats) launch_kfac_ema(raw, stats, K.nstats, ema, s);
+  launch_kfac_invert(K.dev, raw, 1.0 / weight, std::sqrt((double)damping), tr, kbuf, tmp, s);
+  launch_kfac_precondition(K.dev, grad, raw + K.nmat, 1.0 / weight, damping, kbuf, pgrad, nref, info, s);
+  if (params) launch_kfac_update(params, pgrad, nref, info, lr, norm_constraint, s);
+  return check_launch();
 }
 
 int dh_grad_cotangent(const float* diff, const float* nvalid, int B, int part, float* ct, void* stream) {

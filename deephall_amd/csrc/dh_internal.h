@@ -251,4 +251,53 @@ void launch_laughlin(const Dims& d, const float* x, const int* expo, float* logp
 void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                     const float* ct, float* dF, float* jg, int nw, hipStream_t s);
 
+// kfac.hip: KFAC curvature statistics, damped inverses and update (api.cpp dh_kfac_*)
+struct KfacSlot {  // one factor matrix n x n (f32) at float offset `off` of the statistics buffer
+  int n;
+  size_t off;
+};
+struct KfacInvJob {  // one damped inverse: slot, the paired factor's slot (for pi), A or G side
+  int slot, partner, is_a, n;
+  float sqrt_scale;  // sqrt(fixed_scale) of the block
+  size_t gj_off;     // f64 offset of the n x n matrix in the inverse buffer
+};
+struct KfacBlockJob {  // one dense block: gradient segments (ref layout) and f64 work offsets
+  size_t kernel_off;
+  long long bias_off;  // -1: no bias
+  int din, dout;
+  size_t v_off, t_off, pv_off;
+};
+struct KfacGemmJob {  // C[M][N] = A[M][K] B[K][N], f64 offsets into one buffer
+  size_t a_off, b_off, c_off;
+  int M, N, K;
+};
+constexpr int kKfacMaxGen = 80;
+struct KfacGenTable {  // generic (diagonal) parameter segments: ref offset, compact offset
+  int n, total;
+  size_t ref[kKfacMaxGen];
+  int cmp[kKfacMaxGen];
+};
+struct KfacDevPlan {  // device copies of the job tables (owned by the handle)
+  KfacSlot* slots;
+  KfacInvJob* inv_jobs;
+  KfacBlockJob* block_jobs;
+  KfacGemmJob *gemm1, *gemm2;
+  int nslots, njobs, nblocks, nmax, max_v, max_m, max_n;
+  KfacGenTable gen;
+};
+void launch_kfac_aug(const float* P, int nch, int n, float* out, int ld, float scale, float corner, int acc,
+                     hipStream_t s);
+void launch_kfac_feat_gram(const Dims& d, const float* geo, int rows, float* P, hipStream_t s);
+void launch_kfac_fisher_ct(const float* logpsi, int nw, float* ct, hipStream_t s);
+void launch_kfac_generic(const float* fgrad, const KfacGenTable& tab, float* diag, float scale, hipStream_t s);
+void launch_kfac_ema(float* raw, const float* st, size_t n, float ema, hipStream_t s);
+size_t kfac_gj_tmp_doubles(int njobs, int nmax);
+void launch_kfac_invert(const KfacDevPlan& p, const float* raw, double inv_weight, double sqrt_lambda, double* tr,
+                        double* gj, double* tmp, hipStream_t s);
+void launch_kfac_precondition(const KfacDevPlan& p, const float* grad, const float* raw_diag, double inv_weight,
+                              double lambda, double* buf, float* pg, size_t nref, double* info, hipStream_t s);
+void launch_kfac_update(float* params, const float* pg, size_t n, double* info, double lr, double norm_constraint,
+                        hipStream_t s);
+
 }  // namespace dh
+

@@ -1,5 +1,8 @@
 """Run directory, statistics CSV and checkpoints — mirror of deephall/log.py:86-222.
 
+``StatsWriter`` restates the reference's StatsWriter (Copyright 2024-2025 Bytedance Ltd.
+and/or its affiliates, Apache-2.0) to keep its CSV contract.
+
 * ``StatsWriter`` (log.py:86-133): ``train_stats.csv`` with a header row written once
   (appending to an existing non-empty file keeps its header), the same row echoed to
   the log without the hidden fields, ``force_flush`` before checkpoints, the file
@@ -120,6 +123,7 @@ class LogManager:
             self.save_path = Path(f"DeepHall_n{sum(cfg.system.nspins)}l{cfg.system.flux}_{stamp}")
         else:
             self.save_path = Path(cfg.log.save_path)
+        self.explicit_restore = cfg.log.restore_path is not None
         if cfg.log.restore_path is None:
             self.restore_path = self.save_path
         else:
@@ -159,16 +163,29 @@ class LogManager:
             np.savez_compressed(f, **arrays)
 
     def try_restore_checkpoint(self, model, device, opt_init=None):
-        """Newest readable checkpoint in restore_path (or the file itself), else None."""
+        """Newest readable checkpoint in restore_path (or the file itself), else None.
+
+        When ``log.restore_path`` was given explicitly and it holds checkpoints none of
+        which can be read (e.g. a reference checkpoint with its pickled parameter tree,
+        SURVEY.md finding 6), this raises instead of silently starting from random
+        parameters; the implicit restore from ``save_path`` keeps the reference's
+        fall-through (log.py:180-192)."""
         if not self.restore_path.exists():
             return None
         if self.restore_path.is_file():
             return self.restore_checkpoint(self.restore_path, model, device, opt_init)
-        for path in sorted(self.restore_path.glob("ckpt_*.npz"), reverse=True):
+        paths = sorted(self.restore_path.glob("ckpt_*.npz"), reverse=True)
+        errors = []
+        for path in paths:
             try:
                 return self.restore_checkpoint(path, model, device, opt_init)
             except Exception as e:  # noqa: BLE001  (log.py:190: try older checkpoints)
                 logger.warning("Error restoring checkpoint %s: %s", path, e)
+                errors.append(f"{path.name}: {e}")
+        if paths and self.explicit_restore:
+            raise RuntimeError(f"log.restore_path={self.restore_path}: no checkpoint could be restored "
+                               f"({'; '.join(errors)}); checkpoints of this library are flat-key npz files "
+                               f"(INTEGRATION.md §3)")
         return None
 
     @staticmethod

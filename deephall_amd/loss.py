@@ -18,7 +18,7 @@ import torch
 from . import _lib, constants
 from .hamiltonian import _run_local_energy
 from .mcmc import native_network, resolve_network
-from .networks.psiformer import _ptr, _stream, get_handle
+from .networks.psiformer import ParamTree, _ptr, _stream, get_handle
 
 # packed all-reduce: every DH_STAT_* entry (16 floats; the clipped Lz^2 / Lz / L^2 means
 # are 0 unless the penalties are on)
@@ -49,10 +49,16 @@ def device_stats(net, e_l, obs, n_accept=None, steps=1, penalties=False):
     return out
 
 
-def reduce_stats(local: torch.Tensor, raw: bool = False):
+def reduce_stats(local: torch.Tensor, raw: bool = False, flags=None):
     """One all-reduce of the packed device-local stats -> LossStats dict (0-d tensors).
-    ``raw=True`` also returns the reduced packed vector (device, DH_STAT_* layout)."""
-    g = constants.pmean(local[:_NPACK])
+    ``raw=True`` also returns the reduced packed vector (device, DH_STAT_* layout).
+    ``flags``: host floats appended to the packed vector and averaged with it (the driver's
+    checkpoint / signal decisions, so every rank acts on the same value); returned as
+    ``out["flags"]`` (device tensor, the mean over ranks)."""
+    local = local[:_NPACK]
+    if flags:
+        local = torch.cat([local, torch.tensor([float(f) for f in flags], dtype=local.dtype).to(local.device)])
+    g = constants.pmean(local)
     energy = torch.complex(g[0], g[1])
     out = {
         "energy": energy,
@@ -65,6 +71,8 @@ def reduce_stats(local: torch.Tensor, raw: bool = False):
         "angular_momentum_square": g[10],
         "pmove": g[11],
     }
+    if flags:
+        out["flags"] = g[_NPACK:]
     return (out, g) if raw else out
 
 
@@ -93,26 +101,54 @@ def grad_cotangent(diff, nvalid, part=0):
     return ct
 
 
-def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_GRAD):
+def _kfac_buffer(net, device):
+    """[gradient (dh_ref_layout) | curvature statistics] float32, cached per network and
+    device; returns (buffer, number of gradient floats)."""
+    cache = net.__dict__.setdefault("_kfac_buffers", {})
+    if device not in cache:
+        nref = get_handle(net.spec, device).nref
+        cache[device] = (torch.empty(nref + net.kfac_layout(device)["nstats"], dtype=torch.float32, device=device), nref)
+    return cache[device]
+
+
+def make_loss_fn(network, system, mode: LossMode = LossMode.ENERGY_GRAD, curvature: bool = False):
     """loss.py:47-110.  ``loss_and_grad(params, data) -> (LossStats, aux)`` where aux is
     diff [B] complex (ENERGY_DIFF), the real parameter gradient (ENERGY_GRAD, a ParamTree)
     or the complex one ({name: complex tensor}, SR_F_VECTOR).  Every statistic and the
     gradient are averaged over ranks: one packed all-reduce of the statistics, one of the
-    gradient (the reference's Adam path skips the latter, SURVEY.md finding 9)."""
+    gradient (the reference's Adam path skips the latter, SURVEY.md finding 9).
+
+    ``curvature=True`` (ENERGY_GRAD, the KFAC optimizer): the same forward pass also yields
+    the Fisher curvature statistics of the batch — the reference registers
+    ``register_normal_predictive_distribution(Re log psi)`` inside this function (loss.py:98)
+    for kfac_jax to trace — averaged over ranks in the SAME all-reduce as the gradient and
+    left in ``loss_and_grad.curvature`` (float32 [nstats], dh_kfac_layout)."""
     pen = (float(system.lz_penalty), float(system.lz_center), float(system.l2_penalty))
     penalties = pen[0] != 0.0 or pen[2] != 0.0
     if native_network(network) is None:
         return _make_callable_loss_fn(network, system, mode, pen, penalties)
     net = resolve_network(network)
 
-    def loss_and_grad(params, data, n_accept=None, steps=1):
+    def loss_and_grad(params, data, n_accept=None, steps=1, flags=None):
+        """``n_accept`` [B] int (mcmc_step(..., reduce=False).last_n_accept) puts pmove into
+        the packed statistics; ``flags`` rides in the same all-reduce (reduce_stats)."""
         e_l, obs = _run_local_energy(net, params, data)
         local = device_stats(net, e_l, obs, n_accept, steps, penalties=penalties)
-        stats, g = reduce_stats(local, raw=True)
+        stats, g = reduce_stats(local, raw=True, flags=flags)
         loss_and_grad.last = (e_l, obs)
         diff, nvalid = loss_diff(net, e_l, obs, g, *pen)
         if mode == LossMode.ENERGY_DIFF:
             return stats, torch.complex(diff[:, 0], diff[:, 1])
+        if curvature:
+            if mode != LossMode.ENERGY_GRAD:
+                raise ValueError("curvature statistics go with LossMode.ENERGY_GRAD")
+            buf, nref = _kfac_buffer(net, data.device)
+            grad = ParamTree.view_of(net.spec, buf[:nref])
+            curv = buf[nref:]
+            net.kfac_vjp(params, data, grad_cotangent(diff, nvalid, 0), grad, curv)
+            constants.pmean_(buf)  # gradient and curvature statistics: one all-reduce
+            loss_and_grad.curvature = curv
+            return stats, grad
         grad = net.vjp(params, data, grad_cotangent(diff, nvalid, 0))
         constants.pmean_(grad.flat)
         if mode == LossMode.ENERGY_GRAD:
@@ -136,7 +172,7 @@ def _make_callable_loss_fn(f, system, mode, pen, penalties):
         raise TypeError("parameter gradients need a network of this library (Psiformer)")
     e_fn = generic.local_energy(f, system)
 
-    def loss_and_grad(params, data, n_accept=None, steps=1):
+    def loss_and_grad(params, data, n_accept=None, steps=1, flags=None):
         e, o = e_fn(params, data)
         B = e.shape[0]
         e_l = torch.view_as_real(e.to(torch.complex64)).contiguous()
@@ -148,7 +184,7 @@ def _make_callable_loss_fn(f, system, mode, pen, penalties):
         obs[:, 4] = o["angular_momentum_z_square"].float()
         obs[:, 5] = o["angular_momentum_square"].float()
         local = device_stats(None, e_l, obs, n_accept, steps, penalties=penalties)
-        stats, g = reduce_stats(local, raw=True)
+        stats, g = reduce_stats(local, raw=True, flags=flags)
         loss_and_grad.last = (e_l, obs)
         diff, _ = loss_diff(None, e_l, obs, g, *pen)
         return stats, torch.complex(diff[:, 0], diff[:, 1])

@@ -285,7 +285,14 @@ class ParamTree(dict):
     @classmethod
     def zeros(cls, spec: NetworkSpec, device) -> "ParamTree":
         offs = ref_offsets(spec)
-        flat = torch.zeros(offs[-1], dtype=torch.float32, device=device)
+        return cls.view_of(spec, torch.zeros(offs[-1], dtype=torch.float32, device=device))
+
+    @classmethod
+    def view_of(cls, spec: NetworkSpec, flat: torch.Tensor) -> "ParamTree":
+        """A tree of views into an existing flat buffer (dh_ref_layout order)."""
+        offs = ref_offsets(spec)
+        if flat.dim() != 1 or flat.numel() != offs[-1] or flat.dtype != torch.float32:
+            raise ValueError(f"flat buffer must be float32 [{offs[-1]}]")
         t = cls()
         for (name, shape), o in zip(param_shapes(spec).items(), offs):
             t[name] = flat[o : o + int(np.prod(shape))].view(shape)
@@ -424,6 +431,60 @@ class Psiformer:
         _lib.check(h.lib.dh_logpsi_vjp(h.h, _ptr(x), B, _ptr(ct), _ptr(out.flat), _ptr(logpsi), _ptr(ws), ws.numel(),
                                        _stream(x.device)))
         return out
+
+    # ---- KFAC (optimizers/kfac.py:195-241; dh_kfac_*)
+    def kfac_layout(self, device) -> dict:
+        """dh_kfac_layout: statistics size, factor slots and dense blocks."""
+        h = get_handle(self.spec, device)
+        n = h.lib.dh_kfac_layout(h.h, None, 0)
+        if n < 0:
+            _lib.check(n)
+        buf = (C.c_size_t * n)()
+        h.lib.dh_kfac_layout(h.h, buf, n)
+        v = [int(t) for t in buf]
+        nb, ns = v[3], v[2]
+        blocks = [dict(zip(("kernel_seg", "bias_seg", "din", "dout", "a_slot", "g_slot", "scale"), v[6 + 7 * i: 13 + 7 * i]))
+                  for i in range(nb)]
+        for b in blocks:
+            b["scale"] = b["scale"] / 1000.0
+            if b["bias_seg"] >= 2**63:
+                b["bias_seg"] = None
+        o = 6 + 7 * nb
+        slots = [(v[o + 2 * i], v[o + 2 * i + 1]) for i in range(ns)]
+        return {"nstats": v[0], "nmat": v[1], "ngeneric": v[4], "step_ws": v[5], "blocks": blocks, "slots": slots}
+
+    def kfac_vjp(self, params, data: torch.Tensor, ct: torch.Tensor | None, grad: "ParamTree | None",
+                 stats: torch.Tensor, logpsi: torch.Tensor | None = None):
+        """dh_kfac_vjp: one forward pass, the gradient for ``ct`` into ``grad`` (as vjp) and the
+        Fisher curvature statistics of this batch into ``stats`` (float32 [nstats])."""
+        h = self.prepare(params, data.device)
+        x = self._check_walkers(data)
+        B = x.shape[0]
+        if ct is not None:
+            ct = ct.to(device=x.device, dtype=torch.float32).contiguous()
+            if tuple(ct.shape) != (B, 2):
+                raise ValueError(f"cotangents must be [{B}, 2]")
+        need = h.lib.dh_kfac_workspace_bytes(h.h, B)
+        one = h.lib.dh_kfac_workspace_bytes(h.h, 1)
+        ws = h.workspace(max(min(need, VJP_WORKSPACE_BYTES), one))
+        _lib.check(h.lib.dh_kfac_vjp(h.h, _ptr(x), B, _ptr(ct), _ptr(grad.flat) if grad is not None else None,
+                                     _ptr(stats), _ptr(logpsi), _ptr(ws), ws.numel(), _stream(x.device)))
+
+    def kfac_step(self, raw: torch.Tensor, stats: torch.Tensor | None, ema: float, weight: float, grad: "ParamTree",
+                  params: "ParamTree | None", lr: float, damping: float, norm_constraint: float,
+                  pgrad: torch.Tensor, info: torch.Tensor):
+        """dh_kfac_step: EMA of the statistics, damped inverses, P g and (params given) the
+        norm-constrained update in place on ``params.flat``."""
+        dev = grad.flat.device
+        h = get_handle(self.spec, dev)
+        ws = h.kfac_ws if getattr(h, "kfac_ws", None) is not None else None
+        need = self.kfac_layout(dev)["step_ws"] if ws is None else ws.numel()
+        if ws is None:
+            ws = h.kfac_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _lib.check(h.lib.dh_kfac_step(h.h, _ptr(raw), _ptr(stats), float(ema), float(weight), _ptr(grad.flat),
+                                      _ptr(params.flat) if params is not None else None, float(lr), float(damping),
+                                      float(norm_constraint), _ptr(pgrad), _ptr(info), _ptr(ws), ws.numel(),
+                                      _stream(dev)))
 
     # ---- plumbing
     def _check_walkers(self, data: torch.Tensor) -> torch.Tensor:

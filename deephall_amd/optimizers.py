@@ -7,7 +7,10 @@ the loss of ``make_loss_fn(..., ENERGY_GRAD)`` (reverse mode in the HIP library,
 averaged over ranks by the second all-reduce of the iteration — the reference's Adam
 path omits that average, SURVEY.md finding 9); the Adam update is one HIP kernel over
 the flat parameter buffer (``dh_adam_update``, optax.adam semantics).  KFAC
-(optimizers/kfac.py, kfac_jax) is not built on MI355X: asking for it raises.
+(optimizers/kfac.py:195-241 on kfac_jax, the reference's default) runs on the dh_kfac_*
+kernels: the Fisher statistics come out of the gradient's forward pass and share its
+all-reduce, the EMA / damped inverses / preconditioned, norm-constrained update run on the
+device with no host sync (the algorithm is restated in oracle/kfac.py).
 """
 
 from __future__ import annotations
@@ -63,10 +66,63 @@ def make_adam_training_step(cfg: Config, network):
         del key, data
         return AdamState(params)
 
-    def step(state: CheckpointState, key=None):
+    def step(state: CheckpointState, key=None, **stat_kw):
         params, data, opt_state, width = state
-        stats, grads = loss_grad_fn(params, data)
+        stats, grads = loss_grad_fn(params, data, **stat_kw)
         adam_update(params, grads, opt_state, lr_schedule(cfg.optim.adam.lr, opt_state.count))
+        net.invalidate()  # the kernel wrote the flat buffer behind torch's version counter
+        return CheckpointState(params, data, opt_state, width), stats
+
+    return init, step
+
+
+# kfac_jax.Optimizer settings of optimizers/kfac.py:203-218, 230-236
+KFAC_CURVATURE_EMA = 0.95
+KFAC_DAMPING = 1e-3
+KFAC_NORM_CONSTRAINT = 1e-3
+
+
+class KfacState:
+    """The curvature EMA (raw factor sums and their weight) and the step counter of the
+    kfac_jax optimizer state; P g and the step info live beside it on the device."""
+
+    def __init__(self, network, params: ParamTree):
+        dev = params.flat.device
+        lay = network.kfac_layout(dev)
+        self.raw = torch.zeros(lay["nstats"], dtype=torch.float32, device=dev)
+        self.weight = 0.0
+        self.step = 0
+        self.pgrad = torch.zeros_like(params.flat)
+        self.info = torch.zeros(4, dtype=torch.float64, device=dev)
+
+    def state_dict(self):
+        return {"raw": self.raw, "weight": self.weight, "step": self.step}
+
+    def load_state_dict(self, d):
+        self.raw.copy_(torch.as_tensor(d["raw"]))
+        self.weight = float(d["weight"])
+        self.step = int(d["step"])
+
+
+def make_kfac_training_step(cfg: Config, network):
+    """optimizers/kfac.py:195-241: kfac_jax.Optimizer(l2_reg 0, norm_constraint 1e-3,
+    curvature_ema 0.95, inverse_update_period 1, estimation_mode fisher_exact, multi_device)
+    stepped with momentum 0 and damping 1e-3 at the schedule's learning rate."""
+    loss_grad_fn = make_loss_fn(network, cfg.system, LossMode.ENERGY_GRAD, curvature=True)
+    net = loss_grad_fn.network
+
+    def init(params, key=None, data=None):
+        del key, data
+        return KfacState(net, params)
+
+    def step(state: CheckpointState, key=None, **stat_kw):
+        params, data, opt_state, width = state
+        stats, grads = loss_grad_fn(params, data, **stat_kw)
+        opt_state.weight = KFAC_CURVATURE_EMA * opt_state.weight + 1.0
+        lr = lr_schedule(cfg.optim.kfac.lr, opt_state.step)
+        net.kfac_step(opt_state.raw, loss_grad_fn.curvature, KFAC_CURVATURE_EMA, opt_state.weight, grads, params, lr,
+                      KFAC_DAMPING, KFAC_NORM_CONSTRAINT, opt_state.pgrad, opt_state.info)
+        opt_state.step += 1
         net.invalidate()  # the kernel wrote the flat buffer behind torch's version counter
         return CheckpointState(params, data, opt_state, width), stats
 
@@ -79,8 +135,8 @@ def make_inference_step(cfg: Config, network):
     def init(params, key=None, data=None):
         return None
 
-    def step(state: CheckpointState, key=None):
-        stats, _ = loss_fn(state.params, state.data)
+    def step(state: CheckpointState, key=None, **stat_kw):
+        stats, _ = loss_fn(state.params, state.data, **stat_kw)
         return state, stats
 
     return init, step
@@ -95,7 +151,5 @@ def make_optimizer_step(cfg: Config, network):
     if name == OptimizerName.none:
         return make_inference_step(cfg, network)
     if name == OptimizerName.kfac:
-        raise NotImplementedError(
-            "KFAC (optimizers/kfac.py, kfac_jax) is not implemented on MI355X yet: use optim.optimizer=adam or none"
-        )
+        return make_kfac_training_step(cfg, network)
     raise ValueError(f"Optimizer {name} is not implemented!")

@@ -172,19 +172,29 @@ def vmc(cfg: Config, iterations: int | None = None, log=None, burn_in: int | Non
 
 
 class GracefulKiller:
-    """train.py:170-187: SIGINT / SIGTERM set a flag; the loop checkpoints and exits."""
+    """train.py:170-187: SIGINT / SIGTERM set a flag; the loop checkpoints and exits.
+
+    As the reference does, the first signal restores the original handlers (a second
+    Ctrl-C then stops a stuck run); ``restore()`` puts them back when train() returns."""
 
     kill_now = False
 
     def __init__(self):
+        self.original = {}
         try:
-            signal.signal(signal.SIGINT, self.exit_gracefully)
-            signal.signal(signal.SIGTERM, self.exit_gracefully)
+            for sig in (signal.SIGINT, signal.SIGTERM):
+                self.original[sig] = signal.signal(sig, self.exit_gracefully)
         except ValueError:  # not the main thread
-            pass
+            self.original = {}
 
     def exit_gracefully(self, *args):
         self.kill_now = True
+        self.restore()
+
+    def restore(self):
+        for sig, handler in self.original.items():
+            signal.signal(sig, handler)
+        self.original = {}
 
 
 def train(cfg: Config):
@@ -230,35 +240,46 @@ def train(cfg: Config):
     state = CheckpointState(params, data, opt_state, width)
     last_save_time = time.time()
     killer = GracefulKiller()
-    with log_manager.create_writer() as writer:
-        writer.hide("kinetic", "potential", "Lz_square")
-        for step in range(initial_step, cfg.optim.iterations):
-            new_data, pmove = mcmc_step(state.params, state.data, key, state.mcmc_width)
-            key = key.advance(steps)
-            new_width, pmoves = update_mcmc_width(step - initial_step, state.mcmc_width, cfg.mcmc.adapt_frequency,
-                                                  pmove, pmoves)
-            state = state._replace(data=new_data, mcmc_width=new_width)
-            state, stats = training_step(state, None)
-            energy = complex(stats["energy"].item())
-            writer.log(
-                step=str(step),
-                pmove=f"{float(pmove):.2f}",
-                energy=f"{energy.real:.4f}",
-                energy_imag=f"{energy.imag:+.4f}",
-                potential=f"{float(stats['potential']):.4f}",
-                kinetic=f"{complex(stats['kinetic'].item()).real:.4f}",
-                variance=f"{float(stats['variance']):.4f}",
-                Lz=f"{float(stats['angular_momentum_z']):+.4f}",
-                Lz_square=f"{float(stats['angular_momentum_z_square']):.4f}",
-                L_square=f"{float(stats['angular_momentum_square']):.4f}",
-            )
-            now = time.time()
-            nan = bool(np.isnan(energy.real))
-            if ((now - last_save_time > cfg.log.save_time_interval and (step + 1) % cfg.log.save_step_interval == 0)
-                    or nan or step == cfg.optim.iterations - 1 or killer.kill_now):
-                last_save_time = now
-                writer.force_flush()
-                log_manager.save_checkpoint(step, state)
-            if killer.kill_now or nan:
-                raise SystemExit("=" * 30 + " ABORT " + "=" * 30)
+    try:
+        with log_manager.create_writer() as writer:
+            writer.hide("kinetic", "potential", "Lz_square")
+            for step in range(initial_step, cfg.optim.iterations):
+                # mcmc.py:146-147's pmove pmean is folded into the iteration's packed statistics
+                # all-reduce, together with this rank's checkpoint / signal flags: one statistics
+                # all-reduce (+ the gradient's) per iteration, and every rank takes the same
+                # checkpoint decision (save_checkpoint is a collective)
+                new_data, _ = mcmc_step(state.params, state.data, key, state.mcmc_width, reduce=False)
+                n_accept = mcmc_step.last_n_accept
+                key = key.advance(steps)
+                state = state._replace(data=new_data)
+                flags = (time.time() - last_save_time > cfg.log.save_time_interval, killer.kill_now)
+                state, stats = training_step(state, None, n_accept=n_accept, steps=steps, flags=flags)
+                pmove = float(stats["pmove"])
+                time_due, kill_now = (bool(v > 0) for v in stats["flags"].tolist())
+                new_width, pmoves = update_mcmc_width(step - initial_step, state.mcmc_width,
+                                                      cfg.mcmc.adapt_frequency, pmove, pmoves)
+                state = state._replace(mcmc_width=new_width)
+                energy = complex(stats["energy"].item())
+                writer.log(
+                    step=str(step),
+                    pmove=f"{pmove:.2f}",
+                    energy=f"{energy.real:.4f}",
+                    energy_imag=f"{energy.imag:+.4f}",
+                    potential=f"{float(stats['potential']):.4f}",
+                    kinetic=f"{complex(stats['kinetic'].item()).real:.4f}",
+                    variance=f"{float(stats['variance']):.4f}",
+                    Lz=f"{float(stats['angular_momentum_z']):+.4f}",
+                    Lz_square=f"{float(stats['angular_momentum_z_square']):.4f}",
+                    L_square=f"{float(stats['angular_momentum_square']):.4f}",
+                )
+                nan = bool(np.isnan(energy.real))
+                if ((time_due and (step + 1) % cfg.log.save_step_interval == 0)
+                        or nan or step == cfg.optim.iterations - 1 or kill_now):
+                    last_save_time = time.time()
+                    writer.force_flush()
+                    log_manager.save_checkpoint(step, state)
+                if kill_now or nan:
+                    raise SystemExit("=" * 30 + " ABORT " + "=" * 30)
+    finally:
+        killer.restore()
     return state

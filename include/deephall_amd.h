@@ -58,8 +58,13 @@ extern "C" {
 #define DH_ORBITAL_SPARSE 1 /* blocks.py:52-62: 8 features per (j, k) mixed into the M harmonics by
                                lll_weight; folded into the full layout when parameters are set */
 
-/* System + Network fields of deephall/config.py:56-104 that the hot path reads. */
+/* System + Network fields of deephall/config.py:56-104 that the hot path reads.
+ * The first field is the caller's sizeof(dh_config): dh_create rejects any other
+ * value with DH_EINVAL, so a binding written against an older (shorter) layout fails
+ * loudly instead of letting the library read past the caller's struct.  Set it with
+ * DH_CONFIG_INIT or `cfg.struct_size = sizeof(dh_config)`. */
 typedef struct dh_config {
+  uint32_t struct_size;       /* = sizeof(dh_config) = 60 bytes        */
   int n_up, n_dn;             /* System.nspins                          */
   int flux;                   /* System.flux = 2Q                       */
   float radius;               /* System.radius; <= 0 means sqrt(Q)      */
@@ -74,6 +79,7 @@ typedef struct dh_config {
   float excitation_lz;        /* Laughlin: System.lz_center (networks/__init__.py:26) */
   int cf_flux;                /* Laughlin: composite-fermion flux p (laughlin.py:23), >= 1 */
 } dh_config;
+#define DH_CONFIG_INIT {sizeof(dh_config)}
 
 typedef struct dh_handle dh_handle;
 
@@ -137,6 +143,34 @@ int dh_set_params_ref(dh_handle* h, const float* ref, size_t count, void* stream
 size_t dh_vjp_workspace_bytes(const dh_handle* h, int batch);
 int dh_logpsi_vjp(dh_handle* h, const float* x, int B, const float* ct, float* grad, float* logpsi, void* ws,
                   size_t ws_bytes, void* stream);
+/* KFAC — the reference's default optimizer (deephall/optimizers/kfac.py:195-241, kfac_jax
+ * Optimizer with "fisher_exact" curvature, repeated-dense Kronecker blocks, pi-adjusted
+ * damping, norm constraint; restated in oracle/kfac.py).  Orbital "full" only.
+ *
+ * dh_kfac_layout: describes the curvature statistics buffer; returns the number of size_t
+ *   values, writes up to n of them: [0] statistics floats, [1] factor-matrix floats,
+ *   [2] factor slots S, [3] dense blocks nb, [4] generic (diagonal) floats, [5] dh_kfac_step
+ *   workspace bytes, then per block (kernel segment, bias segment or SIZE_MAX, d_in, d_out,
+ *   A slot, G slot, 1000 x fixed scale), then per slot (n, float offset).
+ * dh_kfac_vjp: one forward pass over x [B][N][2] with saved activations, then
+ *   (ct != NULL) the gradient of dh_logpsi_vjp into grad, and the Fisher reverse pass
+ *   (cotangent sqrt(2) on Re log psi; 0 for a walker with non-finite log psi) whose layer
+ *   Gram matrices A = x~^T x~ / rows, G = dy^T dy / rows and generic diagonal
+ *   (sum_b tangent)^2 / B are WRITTEN to stats (this device's batch; average over devices
+ *   before dh_kfac_step).  logpsi [B][2] optional.  Workspace per chunk:
+ *   dh_kfac_workspace_bytes.
+ * dh_kfac_step: raw = ema * raw + stats (stats may be NULL: no EMA update), then with the
+ *   EMA weight `weight` (sum of ema^k): damped inverses, P g into pgrad (dh_ref_layout
+ *   floats), info[0] = <P g, g>, info[1] = c = min(1, sqrt(norm_constraint / (lr^2 <P g, g>))),
+ *   info[2] = lr c (device doubles), and params -= lr c P g when params != NULL. */
+int dh_kfac_layout(dh_handle* h, size_t* out, int n);
+size_t dh_kfac_workspace_bytes(const dh_handle* h, int batch);
+int dh_kfac_vjp(dh_handle* h, const float* x, int B, const float* ct, float* grad, float* stats, float* logpsi,
+                void* ws, size_t ws_bytes, void* stream);
+int dh_kfac_step(dh_handle* h, float* raw, const float* stats, float ema, float weight, const float* grad,
+                 float* params, float lr, float damping, float norm_constraint, float* pgrad, double* info, void* ws,
+                 size_t ws_bytes, void* stream);
+
 /* Cotangents of the gradient estimator 2 nanmean(conj(d log psi) diff) (loss.py:59-64):
  * part 0 (its real part, ENERGY_GRAD): ct = 2 (Re diff, Im diff) / n;
  * part 1 (its imaginary part, SR_F_VECTOR): ct = 2 (Im diff, -Re diff) / n;
@@ -232,7 +266,7 @@ int dh_loss_diff(dh_handle* h, const float* e_l, const float* obs, int B, const 
  * interaction_strength: pe[B]. */
 int dh_potential(dh_handle* h, const float* x, int B, float* pe, void* stream);
 
-/* ---- NetObs-style estimators (deephall/netobs_bridge/observables/*.py) ----------------
+/* ---- NetObs-style estimators (deephall/netobs_bridge/observables/NAME.py) ----------------
  * dh_histograms ADDS to density[density_bins] the counts of every electron's theta and
  * to pair[pair_bins] the 1/sin(theta_12)-weighted counts of every pair angle
  * theta_12 = arccos(r_i . r_j), i < j, both over [0, pi] with numpy's bin rule

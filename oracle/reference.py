@@ -137,8 +137,15 @@ def _layer_norm(x, scale, bias, eps=1e-5):
     return (x - mean) * torch.rsqrt(var + eps) * scale + bias
 
 
-def trunk(params, cfg: OracleConfig, x):
-    """PsiformerLayers.__call__ (psiformer.py:37-60).  x: [N,2] -> [N,D]."""
+def _no_tap(name, x_in, y):
+    return y
+
+
+def trunk(params, cfg: OracleConfig, x, tap=_no_tap):
+    """PsiformerLayers.__call__ (psiformer.py:37-60).  x: [N,2] -> [N,D].
+
+    ``tap(name, x_in, y) -> y`` sees every dense layer's input and output (oracle/kfac.py
+    adds a zero perturbation to read the output tangents, as kfac_jax's layer tags do)."""
     theta, phi = x[..., 0], x[..., 1]
     N = cfg.nelec
     spins = torch.tensor([1.0] * cfg.nspins[0] + [-1.0] * cfg.nspins[1], dtype=x.dtype)
@@ -146,21 +153,22 @@ def trunk(params, cfg: OracleConfig, x):
         [torch.cos(theta), torch.sin(theta) * torch.cos(phi), torch.sin(theta) * torch.sin(phi), spins], -1
     )
     p = "PsiformerLayers_0/"
-    h = feat @ params[p + "Dense_0/kernel"]
+    h = tap(p + "Dense_0", feat, feat @ params[p + "Dense_0/kernel"])
     H, dh = cfg.num_heads, cfg.heads_dim
     for l in range(cfg.num_layers):
         mha = p + f"MultiHeadAttention_{l}/"
-        q = torch.einsum("nd,dhk->nhk", h, params[mha + "query/kernel"]) + params[mha + "query/bias"]
-        k = torch.einsum("nd,dhk->nhk", h, params[mha + "key/kernel"]) + params[mha + "key/bias"]
-        v = torch.einsum("nd,dhk->nhk", h, params[mha + "value/kernel"]) + params[mha + "value/bias"]
+        q = tap(mha + "query", h, torch.einsum("nd,dhk->nhk", h, params[mha + "query/kernel"]) + params[mha + "query/bias"])
+        k = tap(mha + "key", h, torch.einsum("nd,dhk->nhk", h, params[mha + "key/kernel"]) + params[mha + "key/bias"])
+        v = tap(mha + "value", h, torch.einsum("nd,dhk->nhk", h, params[mha + "value/kernel"]) + params[mha + "value/bias"])
         q = q / math.sqrt(dh)
         w = torch.einsum("qhd,khd->hqk", q, k)
         w = torch.softmax(w, dim=-1)
         o = torch.einsum("hqk,khd->qhd", w, v)
-        attn = torch.einsum("qhd,hdD->qD", o, params[mha + "out/kernel"]) + params[mha + "out/bias"]
-        h = h + attn @ params[p + f"Dense_{2 * l + 1}/kernel"]
+        attn = tap(mha + "out", o, torch.einsum("qhd,hdD->qD", o, params[mha + "out/kernel"]) + params[mha + "out/bias"])
+        h = h + tap(p + f"Dense_{2 * l + 1}", attn, attn @ params[p + f"Dense_{2 * l + 1}/kernel"])
         h = _layer_norm(h, params[p + f"LayerNorm_{2 * l}/scale"], params[p + f"LayerNorm_{2 * l}/bias"])
-        h = h + torch.tanh(h @ params[p + f"Dense_{2 * l + 2}/kernel"] + params[p + f"Dense_{2 * l + 2}/bias"])
+        z = tap(p + f"Dense_{2 * l + 2}", h, h @ params[p + f"Dense_{2 * l + 2}/kernel"] + params[p + f"Dense_{2 * l + 2}/bias"])
+        h = h + torch.tanh(z)
         h = _layer_norm(h, params[p + f"LayerNorm_{2 * l + 1}/scale"], params[p + f"LayerNorm_{2 * l + 1}/bias"])
     return h
 
@@ -182,10 +190,10 @@ def envelope(cfg: OracleConfig, theta, phi):
     return norm * upow * vpow
 
 
-def orbitals(params, cfg: OracleConfig, x):
+def orbitals(params, cfg: OracleConfig, x, tap=_no_tap):
     """Psiformer.orbitals (psiformer.py:78-91): [K,N,N] complex, Jastrow included."""
     theta, phi = x[..., 0], x[..., 1]
-    h = trunk(params, cfg, x)
+    h = trunk(params, cfg, x, tap)
     N, K = cfg.nelec, cfg.determinants
     M = int(round(cfg.flux)) + 1
     ob = "Orbitals_0/featured_orbitals/"
@@ -197,12 +205,11 @@ def orbitals(params, cfg: OracleConfig, x):
         if hi - lo == 0:
             continue
         hb = h[lo:hi]
-        re = torch.einsum("nd,dmjk->nmjk", hb, params[ob + f"DenseGeneral_{2 * blk}/kernel"]) + params[
-            ob + f"DenseGeneral_{2 * blk}/bias"
-        ]
-        im = torch.einsum("nd,dmjk->nmjk", hb, params[ob + f"DenseGeneral_{2 * blk + 1}/kernel"]) + params[
-            ob + f"DenseGeneral_{2 * blk + 1}/bias"
-        ]
+        re = tap(ob + f"DenseGeneral_{2 * blk}", hb, torch.einsum(
+            "nd,dmjk->nmjk", hb, params[ob + f"DenseGeneral_{2 * blk}/kernel"]) + params[ob + f"DenseGeneral_{2 * blk}/bias"])
+        im = tap(ob + f"DenseGeneral_{2 * blk + 1}", hb, torch.einsum(
+            "nd,dmjk->nmjk", hb, params[ob + f"DenseGeneral_{2 * blk + 1}/kernel"]) + params[
+                ob + f"DenseGeneral_{2 * blk + 1}/bias"])
         blocks.append(torch.complex(re, im))
         blk += 1
     F = torch.cat(blocks, 0)  # [N, M, N, K]  ("sparse": [N, 8, N, K])
@@ -246,9 +253,9 @@ def jastrow(params, cfg: OracleConfig, x):
     return J
 
 
-def logpsi(params, cfg: OracleConfig, x):
+def logpsi(params, cfg: OracleConfig, x, tap=_no_tap):
     """Psiformer.__call__ (psiformer.py:72-76): complex log psi of one walker x[N,2]."""
-    orb = orbitals(params, cfg, x)
+    orb = orbitals(params, cfg, x, tap)
     sign, logdet = torch.linalg.slogdet(orb)
     logmax = torch.max(logdet)
     return torch.log(torch.sum(sign * torch.exp(logdet - logmax))) + logmax

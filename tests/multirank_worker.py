@@ -1,9 +1,17 @@
 """Rank process of tests/test_gpu_0_multirank.py (not a test module).
 
-One VMC iteration's device work on this rank's contiguous walker shard — mcmc_step with
-its pmove pmean, the local energy, dh_energy_stats and the packed statistics all-reduce —
-with every rank on device 0 and the gloo backend (a one-GPU box; the 8-GPU runs use RCCL).
-Writes the rank's walkers, accept counts and the reduced statistics to argv[1]_<rank>.npz.
+``worker.py OUT [MODE]``, every rank on device 0 with the gloo backend (a one-GPU box;
+the 8-GPU runs use RCCL), writing argv[1]_<rank>.npz:
+
+* ``vmc`` (default): one VMC iteration's device work on this rank's contiguous walker
+  shard — mcmc_step with its pmove pmean, the local energy, dh_energy_stats and the
+  packed statistics all-reduce; the rank's walkers, accept counts and reduced statistics.
+* ``grad``: make_loss_fn(ENERGY_GRAD) on fixed walkers (loss.py:66-108): the statistics
+  all-reduce, the clipped difference, reverse mode and the gradient all-reduce.
+* ``train``: train() (train.py:80-167) with Adam for 2 iterations, checkpoint every
+  step (save_time_interval 0, save_step_interval 1: the collective save decision),
+  the run directory in argv[3]; the final parameters and this rank's walkers.
+* ``nccl``: a world-size-1 "nccl" (RCCL) process group and one all-reduce on the GPU.
 """
 
 from __future__ import annotations
@@ -20,13 +28,78 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def main_grad(out, world, rank):
+    from deephall_amd import config, make_network
+    from deephall_amd.loss import LossMode, make_loss_fn
+    from helpers import make_walkers
+
+    system = config.System(nspins=(6, 0), flux=15)
+    model = make_network(system, config.Network())
+    params = model.init(3, device="cuda")
+    B = 64
+    per = B // world
+    x = torch.tensor(make_walkers(B, 6, seed=5)[rank * per : (rank + 1) * per], device="cuda")
+    stats, grad = make_loss_fn(model, system, LossMode.ENERGY_GRAD)(params, x)
+    torch.cuda.synchronize()
+    np.savez(f"{out}_{rank}.npz", grad=grad.flat.cpu().numpy(), energy=complex(stats["energy"].item()))
+
+
+def main_train(out, world, rank, run_dir):
+    from deephall_amd import Config, train
+
+    cfg = Config.from_dict({
+        "batch_size": 60, "seed": 42,
+        "system": {"nspins": (3, 0), "flux": 2, "interaction_strength": 0.0},
+        "network": {"psiformer": {"num_layers": 1, "num_heads": 1, "heads_dim": 4}},
+        "mcmc": {"burn_in": 4},
+        "optim": {"iterations": 2, "optimizer": "adam", "adam": {"lr": {"rate": 0.02}}},
+        "log": {"save_path": run_dir, "save_time_interval": 0, "save_step_interval": 1},
+    })
+    state = train(cfg)
+    torch.cuda.synchronize()
+    np.savez(f"{out}_{rank}.npz", params=state.params.flat.cpu().numpy(), data=state.data.cpu().numpy(),
+             width=float(state.mcmc_width))
+
+
+def main_nccl(out):
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    from deephall_amd import constants
+
+    t = torch.arange(16, dtype=torch.float32, device="cuda")
+    dist.all_reduce(t)
+    m = constants.pmean(torch.ones(3, device="cuda") * 2.5)
+    torch.cuda.synchronize()
+    np.savez(f"{out}_0.npz", t=t.cpu().numpy(), m=m.cpu().numpy(), backend=dist.get_backend())
+    dist.destroy_process_group()
+
+
 def main():
     out = sys.argv[1]
+    mode = sys.argv[2] if len(sys.argv) > 2 else "vmc"
+    if mode == "nccl":
+        torch.cuda.set_device(0)
+        return main_nccl(out)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     torch.cuda.set_device(0)
     if world > 1:
         dist.init_process_group("gloo")
+    if mode == "grad":
+        main_grad(out, world, rank)
+    elif mode == "train":
+        main_train(out, world, rank, sys.argv[3])
+    else:
+        main_vmc(out, world, rank)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_vmc(out, world, rank):
     from deephall_amd import config, make_network
     from deephall_amd.hamiltonian import _run_local_energy
     from deephall_amd.loss import device_stats, reduce_stats
@@ -50,8 +123,6 @@ def main():
     torch.cuda.synchronize()
     np.savez(f"{out}_{rank}.npz", x=x.cpu().numpy(), n_acc=nacc.cpu().numpy(), mcmc_pmove=float(pmove),
              e_l=e_l.cpu().numpy(), **{k: complex(v.item()) for k, v in stats.items()})
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -179,3 +179,33 @@ def test_param_tree_view_check_tracks_mutations():
     assert t3.is_packed_view(spec)
     t3.pop(name)
     assert not t3.is_packed_view(spec)
+
+
+def test_dh_config_rejects_foreign_layouts():
+    """dh_create checks dh_config.struct_size: the 11-field binding the
+    round-2 INTEGRATION.md showed, and the 14-field layout without struct_size, both fail
+    with DH_EINVAL before any field past the caller's struct is read."""
+    lib = _lib.load()
+    DH_EINVAL = -1
+    assert C.sizeof(_lib.DhConfig) == 60
+
+    class Old11(C.Structure):
+        _fields_ = [(n, C.c_int) for n in ("n_up", "n_dn", "flux")] + [
+            ("radius", C.c_float), ("interaction_strength", C.c_float)] + [
+            (n, C.c_int) for n in ("interaction_type", "num_heads", "heads_dim", "num_layers", "ndets", "orbital_type")]
+
+    class Old14(C.Structure):
+        _fields_ = Old11._fields_ + [("network_type", C.c_int), ("excitation_lz", C.c_float), ("cf_flux", C.c_int)]
+
+    for cls in (Old11, Old14):
+        old = cls(n_up=6, n_dn=0, flux=15, num_heads=4, heads_dim=64, num_layers=2, ndets=1)
+        h = C.c_void_p()
+        assert lib.dh_create(C.cast(C.pointer(old), C.POINTER(_lib.DhConfig)), C.byref(h)) == DH_EINVAL
+        assert b"struct_size" in lib.dh_last_error()
+    cfg = NetworkSpec(nspins=(6, 0), flux=15, ndets=1, num_heads=4, heads_dim=64, num_layers=2).to_c()
+    cfg.struct_size = 56
+    h = C.c_void_p()
+    assert lib.dh_create(C.byref(cfg), C.byref(h)) == DH_EINVAL
+    cfg.struct_size = C.sizeof(_lib.DhConfig)
+    assert lib.dh_create(C.byref(cfg), C.byref(h)) == 0
+    lib.dh_destroy(h)

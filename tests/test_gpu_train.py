@@ -69,7 +69,7 @@ def test_training(cuda, tmp_path, logs):
     # the filled lowest Landau level: E = N/2 = 1.5 exactly (no interaction)
     assert abs(np.mean(e[-30:]) - 1.5) < 0.05, e[-30:]
     text = "\n".join(logs)
-    assert "energy=1.5" in text or "energy=1.4" in text
+    assert "energy=1.5" in text and "energy=1.4" in text  # train_test.py:47-48
 
 
 def test_checkpoint(cuda, tmp_path, logs):
