@@ -166,13 +166,18 @@ class KfacState:
     step: int = 0
 
 
-def update_curvature(state: KfacState, stats, diag, ema=CURVATURE_EMA):
+def update_curvature(state: KfacState, stats, diag, ema=CURVATURE_EMA, storage=None):
+    """``storage=torch.float32`` rounds the EMA sums to float32 (kfac_jax keeps them in
+    the parameters' dtype)."""
+    rnd = (lambda t: t.to(storage).to(DT)) if storage is not None else (lambda t: t)
     for k, (A, G) in stats.items():
-        state.raw_A[k] = ema * state.raw_A.get(k, 0.0) + A
-        state.raw_G[k] = ema * state.raw_G.get(k, 0.0) + G
+        state.raw_A[k] = rnd(ema * state.raw_A.get(k, 0.0) + A)
+        state.raw_G[k] = rnd(ema * state.raw_G.get(k, 0.0) + G)
     for k, d in diag.items():
-        state.raw_d[k] = ema * state.raw_d.get(k, 0.0) + d
+        state.raw_d[k] = rnd(ema * state.raw_d.get(k, 0.0) + d)
     state.weight = ema * state.weight + 1.0
+    if storage is not None:
+        state.weight = float(torch.tensor(state.weight, dtype=storage))
     return state
 
 
@@ -212,10 +217,11 @@ def lr_schedule(t, rate=0.05, decay=1.0, delay=2000.0):
     return rate * (1.0 / (1.0 + t / delay)) ** decay
 
 
-def kfac_step(params, cfg, grads, state: KfacState, stats, diag, lr=None, norm_constraint=NORM_CONSTRAINT):
+def kfac_step(params, cfg, grads, state: KfacState, stats, diag, lr=None, norm_constraint=NORM_CONSTRAINT,
+              storage=None, ema=CURVATURE_EMA):
     """One kfac_jax step given this step's gradient and curvature statistics.  Returns
     (new params, state, info) with info = {"pg": P g, "coef": c, "lr": lr}."""
-    update_curvature(state, stats, diag)
+    update_curvature(state, stats, diag, ema=ema, storage=storage)
     lr = lr_schedule(state.step) if lr is None else lr
     pg = precondition(state, cfg, grads)
     sq = sum(float((pg[k] * grads[k].to(DT)).sum()) for k in pg)
