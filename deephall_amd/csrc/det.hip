@@ -1149,6 +1149,17 @@ __global__ __launch_bounds__(64) void det_bwd_kernel(const float* __restrict__ F
     if (!own) dF[((size_t)b * N + i) * ldF + col] = 0.f;
   }
   const float cr = ct[2 * b], ci = ct[2 * b + 1];
+  if (cr == 0.f && ci == 0.f) {
+    // a walker without weight (NaN diff: the reference's nanmean / nan_to_num drop it,
+    // loss.py:59-64; or psi = 0 in the KFAC Fisher pass): zero rows, so a singular matrix's
+    // inf inverse cannot turn 0 * inf into NaN in every weight gradient
+    for (int idx = tid; idx < N * orb_cols; idx += nt) dF[((size_t)b * N + idx / orb_cols) * ldF + idx % orb_cols] = 0.f;
+    if (tid == 0) {
+      jg[2 * b] = 0.f;
+      jg[2 * b + 1] = 0.f;
+    }
+    return;
+  }
   __syncthreads();
   // Jastrow parameter derivatives (double, reduced over the wave)
   {

@@ -153,3 +153,29 @@ def test_adam_matches_optax_semantics(cuda):
     for k in ref:
         got = params[k].detach().double().cpu()
         assert torch.allclose(got, ref[k], rtol=1e-5, atol=1e-6), k
+
+
+def test_singular_walker_does_not_poison_gradient(cuda):
+    """a walker with two coincident electrons has psi = 0 (two equal orbital
+    rows), a NaN E_L and therefore a zero cotangent (nanmean / nan_to_num drop it,
+    loss.py:59-64).  The reverse pass must skip it — its inverse is inf and 0 * inf would
+    put NaN into every weight gradient — so the gradient equals the one without it."""
+    ocfg = oracle_config("C1")
+    p64 = make_params(ocfg)
+    system, model = build(ocfg)
+    params = to_device_params(p64)
+    x = make_walkers(6, ocfg.nelec, seed=8)
+    x[2, 1] = x[2, 0]  # coincident electrons
+    ct = np.random.default_rng(9).standard_normal((6, 2)).astype(np.float32)
+    ct[2] = 0.0
+    lp = torch.empty(6, 2, device=cuda)
+    g_all = model.vjp(params, torch.tensor(x, device=cuda), torch.tensor(ct, device=cuda), logpsi=lp)
+    assert not np.isfinite(lp[2, 0].item())  # psi = 0 for the coincident walker
+    keep = [0, 1, 3, 4, 5]
+    g_ref = model.vjp(params, torch.tensor(x[keep], device=cuda), torch.tensor(ct[keep], device=cuda))
+    assert torch.isfinite(g_all.flat).all()
+    scale = g_ref.flat.abs().max().item()
+    assert (g_all.flat - g_ref.flat).abs().max().item() <= 1e-6 * scale
+    # through the loss: E_L of that walker is NaN, the gradient stays finite
+    _, grad = make_loss_fn(model, system, LossMode.ENERGY_GRAD)(params, torch.tensor(x, device=cuda))
+    assert torch.isfinite(grad.flat).all()

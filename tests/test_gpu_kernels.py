@@ -73,7 +73,7 @@ def test_gemm_variants(cuda, variant):
             assert torch.isnan(Y[rows:]).all()  # rows past `rows` untouched
 
 
-X6_VARIANTS = [-1, 0, 12, 40, 41, 43, 44, 45, 46, 50, 51, 52, 60, 61, 62]
+X6_VARIANTS = [-1, 0, 12, 40, 41, 43, 44, 45, 46, 50, 51, 52, 56, 57, 60, 61, 62, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 90]
 
 
 def _x6_planes(lib, W, n, K):

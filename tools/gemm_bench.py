@@ -74,7 +74,7 @@ if __name__ == "__main__":
         line = [f"{name:8s}"]
         for v in variants:
             try:
-                ms, tf = run(v, rows, n, k, cc, check=not 290 <= v < 300, residual=name in ("el_d", "fwd_d"))
+                ms, tf = run(v, rows, n, k, cc, check=not (290 <= v < 300 or 286 <= v <= 289), residual=name in ("el_d", "fwd_d"))
                 line.append(f"v{v}: {ms * 1e3:8.1f}us {tf:6.1f}TF")
             except AssertionError as e:
                 line.append(f"v{v}: WRONG {e}")
