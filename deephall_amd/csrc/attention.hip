@@ -786,8 +786,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
     wsync();
     const bool tang = c <= T;
     const int k = c - T - 2;
-    // phase A: scores
-    for (int p = lane; p < 4 * nn; p += 64) {
+    // phase A: scores.  FEAT tangents: channel t moves only electron e = t / 2, so q_t, k_t,
+    // v_t are zero off row e and S_t = s (q_t k0^T + q0 k_t^T) lives on row e and column e
+    // only, P_t = q_t k_t^T on (e, e): 2N dots instead of 3 N^2
+    if (FEAT && tang) {
+      const int e = (c - 1) >> 1;
+      for (int p = lane; p < nn; p += 64) S[p] = P[p] = 0.f;
+      if (lane < 8 * N) {  // task = lane / 4: j < N row e; N + i (i != e) column e; 2N - 1 + ... P
+        const int task = lane >> 2, qt = lane & 3;
+        int i, j;
+        float s1;
+        if (task < N) {  // S[e][j] = qc[e] . k0[j] (+ q0[e] . kc[e] at j = e)
+          i = e;
+          j = task;
+          s1 = dot16(qc + e * ld + 16 * qt, k0 + j * ld + 16 * qt);
+          if (j == e) s1 += dot16(q0 + e * ld + 16 * qt, kc + e * ld + 16 * qt);
+        } else if (task < 2 * N - 1) {  // S[i][e] = q0[i] . kc[e], i != e
+          i = task - N;
+          if (i >= e) ++i;
+          j = e;
+          s1 = dot16(q0 + i * ld + 16 * qt, kc + e * ld + 16 * qt);
+        } else {  // P[e][e]
+          i = j = e;
+          s1 = dot16(qc + e * ld + 16 * qt, kc + e * ld + 16 * qt);
+        }
+        s1 += __shfl_xor(s1, 1, 64);
+        s1 += __shfl_xor(s1, 2, 64);
+        if (qt == 0 && task < 2 * N) {
+          if (task < 2 * N - 1)
+            S[i * N + j] = s1 * scale;
+          else
+            P[i * N + j] = s1;
+        }
+      }
+    }
+    for (int p = lane; p < ((FEAT && tang) ? 0 : 4 * nn); p += 64) {
       const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
       const int oi = i * ld + 16 * qt, oj = j * ld + 16 * qt;
       float s1 = dot16(qc + oi, k0 + oj) + dot16(q0 + oi, kc + oj);

@@ -541,7 +541,9 @@ struct DetSmem {
 // spin block: 2 M N K floats each) fit this many floats.
 constexpr int kStageFloats = 5120;
 __host__ __device__ inline bool det_staged(int N, int M, int K) { return 2 * M * N * K * N <= kStageFloats; }
-__host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
+// pc (the precontracted path): the envelope leaves (E0 .. D2TH) and the flow first-order
+// sums (Gu) are not needed and get no space, so more workgroups fit a CU (C5: 89 -> 33 KiB)
+__host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves, bool pc = false) {
   // offsets in floats; complex arrays take 2 floats per element
   DetSmem L;
   const int T = 2 * N, NN = N * N;
@@ -562,16 +564,17 @@ __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
   L.alpha = o;
   o += 3 * T;
   o = (o + 1) & ~1;
+  const int nm = pc ? 0 : 2 * N * M;
   L.E0 = o;
-  o += 2 * N * M;
+  o += nm;
   L.DTH = o;
-  o += 2 * N * M;
+  o += nm;
   L.DPH = o;
-  o += 2 * N * M;
+  o += nm;
   L.LB = o;
-  o += 2 * N * M;
+  o += nm;
   L.D2TH = o;
-  o += 2 * N * M;
+  o += nm;
   L.Aug = o;
   o += 2 * 2 * NN;
   L.Binv = o;
@@ -583,7 +586,7 @@ __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves) {
   L.Mu = o;
   o += 3 * 2 * NN;
   L.Gu = o;
-  o += 3 * 2 * NN;
+  o += pc ? 0 : 3 * 2 * NN;
   L.fac = o;
   o += 2 * N;
   L.ellt = o;
@@ -622,8 +625,11 @@ __device__ inline void block_sum4(float v[4], float* red) {
 
 // PF > 0: orbital rows staged through LDS, PF floats per thread in flight.
 // PC: the channel matrices come precontracted from env_contract_kernel (PhiC), F unused.
-template <int PF, bool PC = false>
-__global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+// NT: threads per walker, 256 (four waves; the default) or 64 (one wave, DH_DET_WAVE=1:
+// every matrix of N <= 8 has at most 64 entries and a one-wave barrier is nearly free, but
+// the per-walker staging and contraction then run on a quarter of the lanes — slower).
+template <int PF, bool PC = false, int NT = 256>
+__global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                   const float* __restrict__ geo_g, const float* __restrict__ jas,
                                   const float* __restrict__ norm, float* __restrict__ e_l, float* __restrict__ obs,
                                   int N, int n_up, int M, int K, float Q, float radius, float lambda,
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
   extern __shared__ float sm[];
   const int T = 2 * N, C = 2 * N + 5, NN = N * N;
   const int tid = threadIdx.x, nt = blockDim.x;
-  const DetSmem L = det_layout(N, M, K, nt >> 6);
+  const DetSmem L = det_layout(N, M, K, nt >> 6, PC);
   const int b = blockIdx.x;
   float* geo = sm + L.geo;  // st ct sp cp
   float* al = sm + L.alpha;
@@ -750,7 +756,7 @@ __global__ __launch_bounds__(256, 4) void det_energy_kernel(const float* __restr
     }
     for (int idx = tid; idx < 3 * NN; idx += nt) {
       Mu[idx] = cf{0.f, 0.f};
-      Gu[idx] = cf{0.f, 0.f};
+      if (!PC) Gu[idx] = cf{0.f, 0.f};
     }
     __syncthreads();
     eliminate(Aug, 2 * N, N, 2 * N, true, fac, piv, logdet);
@@ -1335,15 +1341,33 @@ bool det_precontract(const Dims& d) {
 
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic) {
-  const int threads = 256;
-  const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64);
-  const size_t bytes = (size_t)L.total * sizeof(float);
+  // DH_DET_WAVE=1: one wave per walker (measured slower: C2 0.60 -> 1.21 ms per step, C5
+  // 13.0 -> 14.0 ms; the per-walker work, not the barriers, dominates — DESIGN.md §7.1)
+  static const bool wave_mode = [] {
+    const char* e = std::getenv("DH_DET_WAVE");
+    return e && e[0] == '1';
+  }();
   const int nrw = 2 * d.M * d.N * d.K * d.N;  // floats of one channel's N staged rows
+  const bool one_wave = wave_mode && 3 * d.N <= 64;
+  const int threads = one_wave ? 64 : 256;
+  const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64, phic != nullptr);
+  const size_t bytes = (size_t)L.total * sizeof(float);
   auto go = [&](auto kern) {
     ensure_smem(kern, bytes);
     hipLaunchKernelGGL(kern, dim3(nw), dim3(threads), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N,
                        d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction, (const float*)phic);
   };
+  if (one_wave && !phic && det_staged(d.N, d.M, d.K)) {
+    if (nrw <= 2 * 64)
+      go(det_energy_kernel<2, false, 64>);
+    else if (nrw <= 6 * 64)
+      go(det_energy_kernel<6, false, 64>);
+    else if (nrw <= 18 * 64)
+      go(det_energy_kernel<18, false, 64>);
+    else
+      go(det_energy_kernel<kStageFloats / 64, false, 64>);
+    return;
+  }
   if (phic) {
     const int G = 64 / d.N;
     const int mgw = (d.M + G - 1) / G;          // harmonics per lane, one wave per electron
@@ -1375,9 +1399,16 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
         default: env(env_contract_kernel<16>, 16, false); break;
       }
     }
-    go(det_energy_kernel<0, true>);
-  } else if (!det_staged(d.N, d.M, d.K))
-    go(det_energy_kernel<0>);
+    if (one_wave)
+      go(det_energy_kernel<0, true, 64>);
+    else
+      go(det_energy_kernel<0, true>);
+  } else if (!det_staged(d.N, d.M, d.K)) {
+    if (one_wave)
+      go(det_energy_kernel<0, false, 64>);
+    else
+      go(det_energy_kernel<0>);
+  }
   else if (nrw <= 8 * threads)
     go(det_energy_kernel<8>);
   else
