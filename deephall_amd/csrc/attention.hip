@@ -891,14 +891,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
             vuj[j] = (k == 0) ? rVu[0][j] : (k == 1 ? rVu[1][j] : rVu[2][j]);
         }
       }
+      // FEAT tangents: v_t lives on row e only, so A0 v_t and sum_j A_t v_t are one term each
+      const int e_t = (c - 1) >> 1;
+      const float vce = (FEAT && tang) ? (VR ? vcreg[VR ? e_t : 0] : vc[e_t * ld + lane]) : 0.f;
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         float acc = 0.f, acc2 = 0.f;
+        if (FEAT && tang) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-          const float r = Rm[i * N + j];
-          acc = fmaf(r, v0r[j], fmaf(A0[i * N + j], vcr[j], acc));
-          if (tang) acc2 = fmaf(r, vcr[j], acc2);
+          for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], v0r[j], acc);
+          acc = fmaf(A0[i * N + e_t], vce, acc);
+          acc2 = Rm[i * N + e_t] * vce;
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            const float r = Rm[i * N + j];
+            acc = fmaf(r, v0r[j], fmaf(A0[i * N + j], vcr[j], acc));
+            if (tang) acc2 = fmaf(r, vcr[j], acc2);
+          }
         }
         if (tang) {
           rOL[i] = fmaf(2.f, acc2, rOL[i]);
