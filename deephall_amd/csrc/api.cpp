@@ -189,17 +189,25 @@ int laughlin_exponents(const dh_config* cfg, std::vector<int>& ex) {
       return fail(DH_EINVAL, "Laughlin quasihole: impossible excitation_lz");
     for (int m = -q2; m < -l2; m += 2) m2.push_back(m);
     for (int m = q2; m > -l2; m -= 2) m2.push_back(m);
-  } else if (N == q2 + 2) {
-    return fail(DH_EINVAL, "Laughlin quasiparticle states (laughlin.py:82-100) are not supported on MI355X yet");
+  } else if (N == q2 + 2) {  // quasiparticle: m = -Q1 .. Q1, then the excited orbital (laughlin.py:82-100)
+    const double lz2 = 2.0 * cfg->excitation_lz;
+    const int l2 = (int)std::lround(lz2);
+    if (std::fabs(lz2 - l2) > 1e-6 || ((l2 - q2) % 2) != 0 || std::abs(l2) > q2 + 2)
+      return fail(DH_EINVAL, "Laughlin quasiparticle: impossible excitation_lz");
+    for (int m = -q2; m <= q2; m += 2) m2.push_back(m);
+    m2.push_back(l2);  // last column: A = Q1 + m1, B = Q1 - m1 (each >= -1)
   } else {
     return fail(DH_EINVAL, "Laughlin: filling not supported");
   }
   if ((int)m2.size() != N) return fail(DH_EINVAL, "Laughlin: orbital count mismatch");
-  ex.assign(2 * N, 0);
+  ex.assign(2 * N + 1, 0);
   for (int j = 0; j < N; ++j) {
     ex[j] = (q2 + m2[j]) / 2;
     ex[N + j] = (q2 - m2[j]) / 2;
   }
+  ex[2 * N] = N == q2 + 2 ? 1 : 0;  // the kernel's quasiparticle flag
+  if (laughlin_smem_bytes(N) > 160 * 1024)
+    return fail(DH_EINVAL, "Laughlin: N too large for the one-workgroup kernel's LDS (160 KiB)");
   return DH_OK;
 }
 }  // namespace

@@ -13,6 +13,22 @@
 // formed in double and fed to the reference's kinetic / angular-momentum formulas
 // (hamiltonian.py:115-169) — the same algorithm as the reference, without autodiff.
 // One 64-thread workgroup per walker, everything in LDS, double precision throughout.
+//
+// Quasiparticle (N = 2 Q1 + 2, laughlin.py:82-100; expo[2N] = 1): columns 0..N-2 are the
+// monomials of m = -Q1..Q1, the last column is the LLL-projected excited orbital.  Its
+// Jastrow factor J_i factors out of row i as for the other states, leaving
+//   X_i = -sum_{k != i} h_ik,  h_ik = (al P1_i u_k + be P2_i v_k) / (u_i v_k - u_k v_i),
+//   P1 = u^A v^(B+1), P2 = u^(A+1) v^B, A = Q1 + m1, B = Q1 - m1, al = A + 1, be = B + 1
+// (laughlin.py:93-99 with the diagonal term of jastrow_dv / jastrow_du cancelled).  That
+// column depends on EVERY electron, so dE_a = e_n rho_a^T + c_a e_L^T (row n = electron of
+// coordinate a, plus the dense column c_a[i] = dX_i / dx_a), and with w_n = E^-1 e_n,
+// y_a = E^-1 c_a, z = row L of E^-1:
+//   tr(E^-1 dE_a)          = rho_a . w_n + y_a[L]
+//   tr(E^-1 dE_a E^-1 dE_b) = (rho_a . w_n')(rho_b . w_n) + (rho_a . y_b) z_n + z_n' (rho_b . y_a)
+//                            + y_a[L] y_b[L]
+//   tr(E^-1 d2E_ab)         = [n = n'] sum_j E^-1[j][n] d2E_nj + sum_i z_i d2X_i / dx_a dx_b
+// with every derivative of h_ik from the quotient rule on its bilinear numerator and
+// denominator (qp_pair).  The ground state and the quasihole are the case c = 0.
 #include "dh_internal.h"
 #include "device_common.h"
 
@@ -38,7 +54,7 @@ __device__ __forceinline__ zd zpow(zd b, int e) {  // e >= 0
 
 // LDS layout (complex doubles unless noted)
 struct LSm {
-  int uv, E, dE, d2E, Einv, R, g, H, misc, total;  // offsets in zd units
+  int uv, E, dE, d2E, Einv, R, g, H, misc, P, c, Y, total;  // offsets in zd units
 };
 __host__ __device__ inline LSm lsm_layout(int N) {
   LSm L;
@@ -61,6 +77,12 @@ __host__ __device__ inline LSm lsm_layout(int N) {
   o += 4 * N * N;
   L.misc = o;
   o += N + 4;  // pivot factors, log det
+  L.P = o;
+  o += 12 * N;  // quasiparticle: P1, P2 of each electron (value, d1[2], d2[3])
+  L.c = o;
+  o += 2 * N * N;  // c[a][i] = dX_i / dx_a
+  L.Y = o;
+  o += 2 * N * N;  // Y[a][j] = (E^-1 c_a)[j]
   L.total = o;
   return L;
 }
@@ -106,6 +128,57 @@ __device__ void monomial(const zd* q, int a, int b, zd* val, zd* d1, zd* d2) {
   }
 }
 
+// h = (al P1_i u_k + be P2_i v_k) / e,  e = u_i v_k - u_k v_i, and its first / second
+// derivatives in the coordinates (0 th_i, 1 ph_i, 2 th_k, 3 ph_k).  qi, qk: uv_derivs of the
+// two electrons; Pi: P1 (0..5) and P2 (6..11) of electron i as value, d/dth, d/dph, d2 tt,
+// tp, pp.  Numerator and denominator are bilinear in (u, v) of the two electrons, so their
+// derivatives are products of uv_derivs terms; h_a = (n_a - h e_a) / e and
+// h_ab = (n_ab - h_a e_b - h_b e_a - h e_ab) / e (the quotient rule twice).
+struct PairD {
+  zd h, d[4], dd[4][4];
+};
+__device__ void qp_pair(const zd* qi, const zd* qk, const zd* Pi, double al, double be, PairD& o) {
+  const zd ui = qi[0], vi = qi[1], uk = qk[0], vk = qk[1];
+  const zd P1 = Pi[0], P2 = Pi[6];
+  // first derivatives of u, v of the electron of coordinate a (0, 1: i; 2, 3: k)
+  auto du = [&](int a) { return a < 2 ? qi[2 + a] : qk[a]; };       // qk[2 + (a - 2)]
+  auto dv = [&](int a) { return a < 2 ? qi[4 + a] : qk[2 + a]; };    // qk[4 + (a - 2)]
+  zd n = al * (P1 * uk) + be * (P2 * vk);
+  zd e = ui * vk - uk * vi;
+  zd na[4], ea[4];
+  for (int a = 0; a < 4; ++a) {
+    if (a < 2) {
+      na[a] = al * (Pi[1 + a] * uk) + be * (Pi[7 + a] * vk);
+      ea[a] = du(a) * vk - uk * dv(a);
+    } else {
+      na[a] = al * (P1 * du(a)) + be * (P2 * dv(a));
+      ea[a] = ui * dv(a) - du(a) * vi;
+    }
+  }
+  const zd einv = zdiv(zd{1.0, 0.0}, e);
+  o.h = n * einv;
+  for (int a = 0; a < 4; ++a) o.d[a] = (na[a] - o.h * ea[a]) * einv;
+  for (int a = 0; a < 4; ++a)
+    for (int b = a; b < 4; ++b) {
+      zd nab, eab;
+      if (b < 2) {  // both on electron i
+        const int k = a + b;  // 0 tt, 1 tp, 2 pp
+        nab = al * (Pi[3 + k] * uk) + be * (Pi[9 + k] * vk);
+        eab = qi[6 + k] * vk - uk * qi[9 + k];
+      } else if (a >= 2) {  // both on electron k
+        const int k = (a - 2) + (b - 2);
+        nab = al * (P1 * qk[6 + k]) + be * (P2 * qk[9 + k]);
+        eab = ui * qk[9 + k] - qk[6 + k] * vi;
+      } else {  // a on i, b on k
+        nab = al * (Pi[1 + a] * du(b)) + be * (Pi[7 + a] * dv(b));
+        eab = du(a) * dv(b) - du(b) * dv(a);
+      }
+      const zd hab = (nab - o.d[a] * ea[b] - o.d[b] * ea[a] - o.h * eab) * einv;
+      o.dd[a][b] = hab;
+      o.dd[b][a] = hab;
+    }
+}
+
 template <bool ENERGY>
 __global__ __launch_bounds__(64) void laughlin_kernel(const float* __restrict__ x, const int* __restrict__ expo,
                                                       float* __restrict__ out_lp, float* __restrict__ e_l,
@@ -116,22 +189,59 @@ __global__ __launch_bounds__(64) void laughlin_kernel(const float* __restrict__ 
   const LSm L = lsm_layout(N);
   zd *UV = sm + L.uv, *E = sm + L.E, *dE = sm + L.dE, *d2E = sm + L.d2E, *Einv = sm + L.Einv, *R = sm + L.R;
   zd *g = sm + L.g, *H = sm + L.H, *fac = sm + L.misc;
+  zd *PP = sm + L.P, *cX = sm + L.c, *Y = sm + L.Y;
   __shared__ int piv;
   __shared__ zd logdet;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int NN = N * N, T = 2 * N;
-  for (int i = tid; i < N; i += nt) uv_derivs((double)x[2 * (b * N + i)], (double)x[2 * (b * N + i) + 1], UV + 12 * i);
+  // quasiparticle: the last column (Lc) is the excited orbital X_i; P1 = u^A v^(B+1) with
+  // weight al = A + 1, P2 = u^(A+1) v^B with be = B + 1 (A or B = -1 only with weight 0)
+  const bool qp = expo[2 * N] != 0;
+  const int Lc = N - 1, qa = expo[N - 1], qb = expo[2 * N - 1];
+  const double al = qa + 1.0, be = qb + 1.0;
+  for (int i = tid; i < N; i += nt) {
+    uv_derivs((double)x[2 * (b * N + i)], (double)x[2 * (b * N + i) + 1], UV + 12 * i);
+    if (qp) {
+      zd* P = PP + 12 * i;
+      for (int t = 0; t < 12; ++t) P[t] = zd{0.0, 0.0};
+      if (al != 0.0) monomial(UV + 12 * i, qa, qb + 1, P, P + 1, P + 3);
+      if (be != 0.0) monomial(UV + 12 * i, qa + 1, qb, P + 6, P + 7, P + 9);
+    }
+  }
   __syncthreads();
-  // E (augmented with I) and its coordinate derivatives (row i depends on electron i only)
+  // E (augmented with I) and its coordinate derivatives (row i depends on electron i only;
+  // the quasiparticle column's derivatives go to cX below, its row entries stay zero)
   for (int idx = tid; idx < NN; idx += nt) {
     const int i = idx / N, j = idx % N;
-    zd val, d1[2], d2[3];
-    monomial(UV + 12 * i, expo[j], expo[N + j], &val, d1, d2);
+    zd val{0.0, 0.0}, d1[2] = {{0.0, 0.0}, {0.0, 0.0}}, d2[3] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+    if (!qp || j != Lc) monomial(UV + 12 * i, expo[j], expo[N + j], &val, d1, d2);
+    if (qp && j == Lc) val = zd{0.0, 0.0};  // X_i: the pair pass below
     E[i * 2 * N + j] = val;
     E[i * 2 * N + N + j] = zd{i == j ? 1.0 : 0.0, 0.0};
     dE[idx] = d1[0];
     dE[NN + idx] = d1[1];
     for (int k = 0; k < 3; ++k) d2E[k * NN + idx] = d2[k];
+  }
+  __syncthreads();
+  if (qp) {
+    // X_i and c[a][i] = dX_i / dx_a (thread i owns column i of c)
+    for (int i = tid; i < N; i += nt) {
+      for (int a = 0; a < T; ++a) cX[a * N + i] = zd{0.0, 0.0};
+      zd X{0.0, 0.0}, own0{0.0, 0.0}, own1{0.0, 0.0};
+      for (int k = 0; k < N; ++k) {
+        if (k == i) continue;
+        PairD pd;
+        qp_pair(UV + 12 * i, UV + 12 * k, PP + 12 * i, al, be, pd);
+        X = X - pd.h;
+        own0 = own0 - pd.d[0];
+        own1 = own1 - pd.d[1];
+        cX[(2 * k) * N + i] = zd{0.0, 0.0} - pd.d[2];
+        cX[(2 * k + 1) * N + i] = zd{0.0, 0.0} - pd.d[3];
+      }
+      cX[(2 * i) * N + i] = own0;
+      cX[(2 * i + 1) * N + i] = own1;
+      E[i * 2 * N + Lc] = X;
+    }
   }
   if (tid == 0) logdet = zd{0.0, 0.0};
   __syncthreads();
@@ -206,10 +316,53 @@ __global__ __launch_bounds__(64) void laughlin_kernel(const float* __restrict__ 
     R[idx] = s;
   }
   __syncthreads();
+  if (qp) {
+    // Y[a][j] = (E^-1 c_a)[j]; H <- T2[a][b] = sum_i z_i d2X_i / dx_a dx_b, z = row Lc of E^-1:
+    // thread per electron block (n, n'): n = n' sums the own-own terms of the pairs (n, k)
+    // and the other-other terms of the pairs (k, n); n != n' takes the cross terms of the
+    // pairs (n, n') and (n', n)
+    for (int idx = tid; idx < T * N; idx += nt) {
+      const int a = idx / N, j = idx % N;
+      zd s{0.0, 0.0};
+      for (int i = 0; i < N; ++i) s = s + Einv[j * N + i] * cX[a * N + i];
+      Y[idx] = s;
+    }
+    for (int blk = tid; blk < NN; blk += nt) {
+      const int n = blk / N, n2 = blk % N;
+      zd t[2][2] = {{{0.0, 0.0}, {0.0, 0.0}}, {{0.0, 0.0}, {0.0, 0.0}}};
+      PairD pd;
+      if (n == n2) {
+        for (int k = 0; k < N; ++k) {
+          if (k == n) continue;
+          qp_pair(UV + 12 * n, UV + 12 * k, PP + 12 * n, al, be, pd);  // X_n: n own
+          const zd zn = Einv[Lc * N + n];
+          for (int x2 = 0; x2 < 2; ++x2)
+            for (int y2 = 0; y2 < 2; ++y2) t[x2][y2] = t[x2][y2] - zn * pd.dd[x2][y2];
+          qp_pair(UV + 12 * k, UV + 12 * n, PP + 12 * k, al, be, pd);  // X_k: n other
+          const zd zk = Einv[Lc * N + k];
+          for (int x2 = 0; x2 < 2; ++x2)
+            for (int y2 = 0; y2 < 2; ++y2) t[x2][y2] = t[x2][y2] - zk * pd.dd[2 + x2][2 + y2];
+        }
+      } else {
+        qp_pair(UV + 12 * n, UV + 12 * n2, PP + 12 * n, al, be, pd);  // X_n: (own n, other n2)
+        const zd zn = Einv[Lc * N + n];
+        for (int x2 = 0; x2 < 2; ++x2)
+          for (int y2 = 0; y2 < 2; ++y2) t[x2][y2] = t[x2][y2] - zn * pd.dd[x2][2 + y2];
+        qp_pair(UV + 12 * n2, UV + 12 * n, PP + 12 * n2, al, be, pd);  // X_n2: (own n2, other n)
+        const zd zm = Einv[Lc * N + n2];
+        for (int x2 = 0; x2 < 2; ++x2)
+          for (int y2 = 0; y2 < 2; ++y2) t[x2][y2] = t[x2][y2] - zm * pd.dd[2 + x2][y2];
+      }
+      for (int x2 = 0; x2 < 2; ++x2)
+        for (int y2 = 0; y2 < 2; ++y2) H[(2 * n + x2) * T + 2 * n2 + y2] = t[x2][y2];
+    }
+    __syncthreads();
+  }
   // gradient: determinant + pairs
   for (int a = tid; a < T; a += nt) {
     const int e = a >> 1, c = a & 1;
     zd s = R[a * N + e];
+    if (qp) s = s + Y[a * N + Lc];
     const zd* qe = UV + 12 * e;
     for (int j = 0; j < N; ++j) {
       if (j == e) continue;
@@ -224,6 +377,15 @@ __global__ __launch_bounds__(64) void laughlin_kernel(const float* __restrict__ 
   for (int idx = tid; idx < T * T; idx += nt) {
     const int a = idx / T, bb = idx % T, ea = a >> 1, ca = a & 1, eb = bb >> 1, cb = bb & 1;
     zd h = zd{0.0, 0.0} - R[bb * N + ea] * R[a * N + eb];
+    if (qp) {
+      // T2 (left in H by the pass above) - (rho_a . y_b) z_ea - z_eb (rho_b . y_a) - y_a[L] y_b[L]
+      zd sab{0.0, 0.0}, sba{0.0, 0.0};
+      for (int j = 0; j < N; ++j) {
+        sab = sab + dE[ca * NN + ea * N + j] * Y[bb * N + j];
+        sba = sba + dE[cb * NN + eb * N + j] * Y[a * N + j];
+      }
+      h = h + H[idx] - sab * Einv[Lc * N + ea] - Einv[Lc * N + eb] * sba - Y[a * N + Lc] * Y[bb * N + Lc];
+    }
     const zd* qa = UV + 12 * ea;
     if (ea == eb) {
       const int k = ca + cb;  // 0 tt, 1 tp, 2 pp

@@ -3,17 +3,15 @@
 from __future__ import annotations
 
 from ..config import Network, NetworkType, System
-from .laughlin import Laughlin, LaughlinQuasiparticle, laughlin_q1
+from .laughlin import Laughlin, LaughlinQuasiparticle
 from .psiformer import Psiformer
 
 
 def make_network(system: System, network: Network) -> Psiformer:
     Q = system.flux / 2
     ntype = str(getattr(network.type, "value", network.type))
-    if ntype == NetworkType.laughlin.value:  # networks/__init__.py:24-27
-        if sum(system.nspins) == 2 * laughlin_q1(system.nspins, system.flux) + 2:  # quasiparticle filling
-            return LaughlinQuasiparticle(flux=system.flux, nspins=system.nspins, excitation_lz=system.lz_center,
-                                         system=system)
+    if ntype == NetworkType.laughlin.value:  # networks/__init__.py:24-27 (ground state, quasihole and
+        # quasiparticle fillings all run on laughlin.hip)
         return Laughlin(flux=system.flux, nspins=system.nspins, excitation_lz=system.lz_center, system=system)
     if ntype == NetworkType.psiformer.value:
         return Psiformer(

@@ -2,17 +2,18 @@
 
 ``Laughlin(nspins, flux, cf_flux=1, excitation_lz=0)`` (the reference module's fields;
 networks/__init__.py:25-27 passes ``System.lz_center`` as ``excitation_lz``): the
-ground state (N = 2 Q1 + 1) and the quasihole state (N = 2 Q1), Q1 = flux/2 - p (N - 1).
+ground state (N = 2 Q1 + 1), the quasihole state (N = 2 Q1) and the quasiparticle state
+(N = 2 Q1 + 2, laughlin.py:82-100), Q1 = flux/2 - p (N - 1).
 It has no parameters: ``init`` returns an empty tree.  ``apply`` is batched log psi
 (dh_logpsi); the MCMC step and the local energy run the HIP kernels of laughlin.hip
 through the same entry points as the Psiformer (make_mcmc_step, local_energy,
-make_local_kinetic_energy), with the full analytic Hessian in double precision.
-The quasiparticle state (N = 2 Q1 + 2, laughlin.py:82-100) is `LaughlinQuasiparticle`: its
-LLL-projected excited orbital depends on every electron through the Jastrow derivatives, so
-it is not a Slater determinant of one-electron orbitals and is evaluated as a log-psi
-callable (the reference's own form, slogdet of the orbital matrix) through the library's
-callable boundary (deephall_amd.generic: derivatives by torch.func, proposal / accept and
-the KE / Lz / L^2 assembly in HIP).
+make_local_kinetic_energy), with the full analytic Hessian in double precision.  The
+quasiparticle's LLL-projected excited orbital depends on every electron through the
+Jastrow derivatives; laughlin.hip carries that column's dense derivatives through the
+determinant algebra (see the kernel's header).
+`LaughlinQuasiparticle` is the same state as a plain log-psi callable (the reference's own
+slogdet form, evaluated through the library's callable boundary, deephall_amd.generic:
+torch.func derivatives): a second, independent route the tests compare the kernel with.
 """
 
 from __future__ import annotations

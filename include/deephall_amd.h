@@ -53,7 +53,7 @@ extern "C" {
 #define DH_INTERACTION_COULOMB 0
 #define DH_INTERACTION_HARMONIC 1
 #define DH_NETWORK_PSIFORMER 0
-#define DH_NETWORK_LAUGHLIN 1 /* networks/laughlin.py: ground state and quasihole (no parameters) */
+#define DH_NETWORK_LAUGHLIN 1 /* networks/laughlin.py: ground state, quasihole, quasiparticle (no parameters) */
 #define DH_ORBITAL_FULL 0
 #define DH_ORBITAL_SPARSE 1 /* blocks.py:52-62: 8 features per (j, k) mixed into the M harmonics by
                                lll_weight; folded into the full layout when parameters are set */

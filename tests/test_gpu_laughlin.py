@@ -5,8 +5,9 @@
   Hessian through hamiltonian.py's formulas); the kernels work in double, so 1e-5.
 * Analytic pins on every walker of a full batch: the Laughlin ground state lies in the
   lowest Landau level with L = 0 (KE = N/2, L^2 = Lz = 0); the quasihole has L = Q1
-  (L^2 = Q1 (Q1 + 1), Lz = excitation_lz); the quasiparticle (laughlin.py:82-100, through
-  the callable boundary) has L = Q1 + 1 = N/2.
+  (L^2 = Q1 (Q1 + 1), Lz = excitation_lz); the quasiparticle (laughlin.py:82-100) has
+  L = Q1 + 1 = N/2 — on the native kernel and, as an independent route, on the reference's
+  slogdet form through the callable boundary (torch.func derivatives).
 * The reference's CLI test restated (tests/cli_test.py:24-42): Laughlin N=3, 2Q=6,
   Coulomb, optimizer none, 100 iterations, seed 42, batch 3360 -> the energy log shows
   2.58 and L_square=0.0000.
@@ -28,7 +29,12 @@ from oracle import reference as R
 pytestmark = pytest.mark.gpu
 CASES = [dict(nspins=(3, 0), flux=6), dict(nspins=(5, 0), flux=12), dict(nspins=(4, 0), flux=10, excitation_lz=0.0),
          dict(nspins=(4, 0), flux=10, excitation_lz=1.0), dict(nspins=(2, 1), flux=6, interaction_type="harmonic"),
-         dict(nspins=(3, 0), flux=6, radius=2.0)]
+         dict(nspins=(3, 0), flux=6, radius=2.0),
+         # quasiparticle fillings N = 2 Q1 + 2 (laughlin.py:82-100): lz = -2 / 2 are the edge
+         # orbitals whose u^(Q1+m1) / v^(Q1-m1) exponent is -1 (its weight Q1 + 1 -+ m1 is 0)
+         dict(nspins=(4, 0), flux=8, excitation_lz=1.0), dict(nspins=(4, 0), flux=8, excitation_lz=-2.0),
+         dict(nspins=(4, 0), flux=8, excitation_lz=2.0), dict(nspins=(6, 0), flux=14, excitation_lz=0.0),
+         dict(nspins=(3, 2), flux=11, excitation_lz=0.5, interaction_type="harmonic")]
 
 
 def build(case):
@@ -78,22 +84,27 @@ def test_laughlin_analytic_pins(cuda, case, L2):
         assert np.max(err) < 1e-6, (k, np.max(err))
 
 
-@pytest.mark.parametrize("N,lz", [(4, 0.0), (4, 1.0), (4, -2.0), (6, 1.0)])
-def test_quasiparticle_analytic_pins(cuda, N, lz):
+@pytest.mark.parametrize("N,lz,B", [(4, 0.0, 4096), (4, 1.0, 4096), (4, -2.0, 4096), (4, 2.0, 4096), (6, 1.0, 4096),
+                                    (8, -1.0, 1024), (10, 0.0, 512)])
+def test_quasiparticle_analytic_pins(cuda, N, lz, B):
     """laughlin.py:82-100 (N = 2 Q1 + 2, 2Q = 3 (N - 1) - 1): the LLL-projected quasiparticle
     is a lowest-Landau-level state (KE = N/2 on every walker) with L = Q1 + 1 = N/2 and
-    Lz = excitation_lz, evaluated through the callable boundary (torch.func derivatives of
-    the reference's slogdet form, KE / Lz / L^2 assembled by dh_kinetic_from_derivatives)."""
-    from deephall_amd.networks import LaughlinQuasiparticle
+    Lz = excitation_lz — on every walker of a batch, through the native kernel (laughlin.hip,
+    make_network's model), and on the first 128 walkers also through the callable boundary
+    (torch.func derivatives of the reference's slogdet form, `LaughlinQuasiparticle`): the
+    two routes agree to 1e-6 relative on log psi and to 1e-5 (relative to the size of the
+    cancelling magnetic terms, as the pins) on every observable."""
+    from deephall_amd.networks import Laughlin, LaughlinQuasiparticle
 
     flux = 3 * (N - 1) - 1
     system = config.System(nspins=(N, 0), flux=flux, lz_center=lz)
     net = config.Network()
     net.type = config.NetworkType.laughlin
     model = make_network(system, net)
-    assert isinstance(model, LaughlinQuasiparticle) and model.Q1 == (N - 2) / 2
-    x = torch.tensor(make_walkers(256, N, seed=5, margin=0.05), device=cuda)
-    e, o = hamiltonian.local_energy(model, system)(model.init(), x)
+    assert isinstance(model, Laughlin)
+    x = torch.tensor(make_walkers(B, N, seed=5, margin=0.05), device=cuda)
+    params = model.init(0, device=cuda)
+    e, o = hamiltonian.local_energy(model, system)(params, x)
     L = N / 2
     st = torch.sin(x[..., 0].double().cpu())
     geo = ((flux / 2) ** 2 * (1 / st).sum(-1) ** 2).numpy()  # size of the cancelling magnetic terms
@@ -102,6 +113,20 @@ def test_quasiparticle_analytic_pins(cuda, N, lz):
         err = np.abs(o[k].real.cpu().numpy() - want) / np.maximum(1.0, geo)
         assert np.max(err) < 1e-5, (k, np.max(err))
     assert np.max(np.abs(o["kinetic"].imag.cpu().numpy()) / np.maximum(1.0, geo)) < 1e-5
+    # the callable route on the same walkers
+    qp = LaughlinQuasiparticle(flux=flux, nspins=(N, 0), excitation_lz=lz, system=system)
+    assert qp.Q1 == (N - 2) / 2
+    xs = x[:128].contiguous()
+    lp_native = model.apply(params, xs).cpu().numpy()
+    lp_callable = qp(None, xs).cpu().numpy()
+    assert np.max(np.abs(lp_native.real - lp_callable.real) / np.maximum(1, np.abs(lp_callable.real))) < 1e-6
+    assert np.max(np.abs(np.angle(np.exp(1j * (lp_native.imag - lp_callable.imag))))) < 1e-5
+    e2, o2 = hamiltonian.local_energy(qp, system)(qp.init(), xs)
+    for k in ("kinetic", "potential", "angular_momentum_z", "angular_momentum_z_square", "angular_momentum_square"):
+        a, r = o[k][:128].cpu().numpy(), o2[k].cpu().numpy()
+        err = np.abs(a - r) / np.maximum(np.maximum(1.0, np.abs(r)), geo[:128])
+        print(f"N={N} lz={lz} {k}: native vs callable {np.max(err):.1e}")
+        assert np.max(err) < 1e-5, (k, np.max(err))
 
 
 def test_quasiparticle_mcmc(cuda):
@@ -122,7 +147,7 @@ def test_quasiparticle_mcmc(cuda):
     assert 0.05 < pm <= 1.0, pm
     assert torch.isfinite(x).all()
     assert (x[..., 0] >= 0).all() and (x[..., 0] <= np.pi).all()
-    lp = model(None, x)
+    lp = model.apply(model.init(0, device=cuda), x)
     assert torch.isfinite(lp.real).all()
 
 
