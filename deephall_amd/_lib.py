@@ -7,6 +7,7 @@ there is no CPU / PyTorch fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdeephall_amd.so"
@@ -113,7 +114,8 @@ def load(path: Path | str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # DH_LIB_PATH: an alternative build of the same library (A/B timing tools only)
+    p = Path(path) if path else Path(os.environ.get("DH_LIB_PATH") or LIB_PATH)
     if not p.exists():
         raise RuntimeError(
             f"deephall_amd HIP library not found at {p}. Build it with "

@@ -11,6 +11,8 @@
 //            o_Sk = A_Sk v0 + A0 v_Sk + 2 (sum_t alpha_kt A_t)(sum_t alpha_kt v_t)
 //
 // qkv rows are (walker, electron, channel); columns [q | k | v], head h at h*dh.
+#include <type_traits>
+
 #include "dh_internal.h"
 #include "device_common.h"
 #include "attn_val.h"
@@ -779,7 +781,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
     return make_float4(-ae * st, ae * ct * cp - ao * sp, ae * ct * sp + ao * cp, 0.f);
   };
 
-  for (int c = 1; c < C; ++c) {
+  // one channel c >= 1 (the loops below run the tangents, then the Laplacian and flow
+  // channels, with the flow products in between: each loop sees a fixed channel kind)
+  auto chan = [&](const int c) __attribute__((always_inline)) {
     wsync();
     commit(qc, kc, vc, vcreg);
     if (c + 1 < C) prefetch(c + 1);
@@ -820,26 +824,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
         }
       }
     }
-    for (int p = lane; p < ((FEAT && tang) ? 0 : 4 * nn); p += 64) {
-      const int pair = p >> 2, qt = p & 3, i = pair / N, j = pair - (pair / N) * N;
-      const int oi = i * ld + 16 * qt, oj = j * ld + 16 * qt;
-      float s1 = dot16(qc + oi, k0 + oj) + dot16(q0 + oi, kc + oj);
-      float s2 = tang ? dot16(qc + oi, kc + oj) : 0.f;
-      s1 += __shfl_xor(s1, 1, 64);
-      s1 += __shfl_xor(s1, 2, 64);
-      s2 += __shfl_xor(s2, 1, 64);
-      s2 += __shfl_xor(s2, 2, 64);
-      if (qt == 0) {
+    // dense channels: lane = (row i, group of JB columns j, quarter of d): the q rows of i
+    // are read once per JB pairs (N = 6: one pass of 48 lanes, 32 b128 reads per lane where
+    // one pair per lane took three passes of 24)
+    constexpr int JB = 3, NG = (N + JB - 1) / JB;
+    for (int p = lane; p < ((FEAT && tang) ? 0 : 4 * N * NG); p += 64) {
+      const int qt = p & 3, ig = p >> 2, i = ig / NG, j0 = (ig - (ig / NG) * NG) * JB;
+      const float* qci = qc + i * ld + 16 * qt;
+      const float* q0i = q0 + i * ld + 16 * qt;
+      float s1[JB], s2[JB];
+#pragma unroll
+      for (int jj = 0; jj < JB; ++jj) s1[jj] = s2[jj] = 0.f;
+#pragma unroll 1
+      for (int m = 0; m < 4; ++m) {  // rolled: the live running sums leave few registers
+        const float4 a = *reinterpret_cast<const float4*>(qci + 4 * m);
+        const float4 a0 = *reinterpret_cast<const float4*>(q0i + 4 * m);
+#pragma unroll
+        for (int jj = 0; jj < JB; ++jj) {
+          if (N % JB != 0 && j0 + jj >= N) continue;
+          const int oj = (j0 + jj) * ld + 16 * qt + 4 * m;
+          const float4 b0 = *reinterpret_cast<const float4*>(k0 + oj);
+          const float4 bc = *reinterpret_cast<const float4*>(kc + oj);
+          s1[jj] = fmaf(a.x, b0.x, fmaf(a.y, b0.y, fmaf(a.z, b0.z, fmaf(a.w, b0.w, s1[jj]))));
+          s1[jj] = fmaf(a0.x, bc.x, fmaf(a0.y, bc.y, fmaf(a0.z, bc.z, fmaf(a0.w, bc.w, s1[jj]))));
+          if (tang) s2[jj] = fmaf(a.x, bc.x, fmaf(a.y, bc.y, fmaf(a.z, bc.z, fmaf(a.w, bc.w, s2[jj]))));
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < JB; ++jj) {
+        s1[jj] += __shfl_xor(s1[jj], 1, 64);
+        s1[jj] += __shfl_xor(s1[jj], 2, 64);
         if (tang) {
-          S[pair] = s1 * scale;
-          P[pair] = s2;
-        } else if (k < 0) {
-          S[pair] = s1 * scale + accS[pair];
-          P[pair] = T2[pair];
-        } else {
-          S[pair] = scale * (s1 + 2.f * QK[k * nn + pair]);
-          const float u = SuB[k * nn + pair];
-          P[pair] = u * u;
+          s2[jj] += __shfl_xor(s2[jj], 1, 64);
+          s2[jj] += __shfl_xor(s2[jj], 2, 64);
+        }
+      }
+      if (qt == 0) {
+#pragma unroll
+        for (int jj = 0; jj < JB; ++jj) {
+          if (N % JB != 0 && j0 + jj >= N) continue;
+          const int pair = i * N + j0 + jj;
+          if (tang) {
+            S[pair] = s1[jj] * scale;
+            P[pair] = s2[jj];
+          } else if (k < 0) {
+            S[pair] = s1[jj] * scale + accS[pair];
+            P[pair] = T2[pair];
+          } else {
+            S[pair] = scale * (s1[jj] + 2.f * QK[k * nn + pair]);
+            const float u = SuB[k * nn + pair];
+            P[pair] = u * u;
+          }
         }
       }
     }
@@ -934,16 +969,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
         obase[(size_t)(i * C + c) * D] = acc;
       }
     }
-    if (c == T) {  // last tangent: qu_k . ku_k^T for the flow channels
+  };
+  for (int c = 1; c <= T; ++c) chan(c);
+  {  // after the last tangent: qu_k . ku_k^T for the flow channels
+      // sums over the 64 lanes of R per-lane values, 8 at a time transposed through the
+      // current channel's q|k|v rows (free until the next commit): 8 writes, 2 b128 reads
+      // and 3 swaps per 8 sums, where a butterfly costs 6 ds_bpermute per sum.  TSUM: those
+      // rows hold the [8][68] scratch
+      constexpr bool TSUM = (VR ? 2 : 3) * N * ld >= 8 * 68;
+      float* tw = qc;  // [8][68]
+      auto lane_sums = [&](auto getv, auto R_, float* dst) __attribute__((always_inline)) {
+        constexpr int R = decltype(R_)::value, HS = 8;  // rows per pass (8 lanes per row)
+        wsync();
+#pragma unroll
+        for (int r0 = 0; r0 < R; r0 += HS) {
+#pragma unroll
+          for (int j = 0; j < HS; ++j)
+            if (r0 + j < R) tw[j * 68 + lane] = getv(r0 + j);
+          wsync();
+          const int jr = lane >> 3, q = lane & 7;
+          const float4 t0 = *reinterpret_cast<const float4*>(tw + jr * 68 + 8 * q);
+          const float4 t1 = *reinterpret_cast<const float4*>(tw + jr * 68 + 8 * q + 4);
+          float v = ((t0.x + t0.y) + (t0.z + t0.w)) + ((t1.x + t1.y) + (t1.z + t1.w));
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          if (q == 0 && r0 + jr < R) dst[r0 + jr] = v;
+          wsync();
+        }
+      };
       if constexpr (FEAT) {
-        // 4 x 4 Wq Wk^T of this head (wave reductions over the head's 64 columns)
+        // 4 x 4 Wq Wk^T of this head (sums over the head's 64 columns), through QK's slots
         const float wq[4] = {fw.wq.x, fw.wq.y, fw.wq.z, fw.wq.w};
         const float wk[4] = {fw.wk.x, fw.wk.y, fw.wk.z, fw.wk.w};
         float Mqk[4][4];
+        if constexpr (TSUM) {
+          lane_sums([&](int r) { return wq[r >> 2] * wk[r & 3]; }, std::integral_constant<int, 16>{}, QK);
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+          for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) Mqk[a][e] = wave_sum(wq[a] * wk[e]);
+            for (int e = 0; e < 4; ++e) Mqk[a][e] = QK[4 * a + e];
+          wsync();
+        } else {
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Mqk[a][e] = wave_sum(wq[a] * wk[e]);
+        }
         for (int p = lane; p < 3 * nn; p += 64) {
           const int kk = p / nn, pair = p - kk * nn, i = pair / N, j = pair - (pair / N) * N;
           const float4 gi_ = gflow(kk, i), gj = gflow(kk, j);
@@ -955,6 +1027,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
             for (int e = 0; e < 4; ++e) v = fmaf(gia[a] * Mqk[a][e], gja[e], v);
           QK[p] = v;
         }
+      } else if constexpr (TSUM) {
+        // one pass per (k, i): the N products qu_k[i] ku_k[j] (compile-time register indices)
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+          for (int i = 0; i < N; ++i)
+            lane_sums([&](int j) { return rQu[kk][i] * rKu[kk][j]; }, std::integral_constant<int, N>{},
+                      QK + kk * nn + i * N);
       } else {
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk)
@@ -966,8 +1046,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(N <= 8 ? 3 :
               if (lane == 0) QK[kk * nn + i * N + j] = v;
             }
       }
-    }
   }
+#pragma unroll
+  for (int c = T + 1; c < C; ++c) chan(c);  // unrolled: the flow index k is a constant
 }
 
 // ---------------------------------------------------------------------------------------

@@ -17,6 +17,7 @@ SHAPES = {
     "fwd_orb": (24576, 192, 256, 1),
     "el_qkv": (417792, 768, 256, 17),
     "el_d": (417792, 256, 256, 17),
+    "el_m": (417792, 256, 256, 17),
     "el_orb": (417792, 192, 256, 17),
 }
 
