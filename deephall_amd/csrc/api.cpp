@@ -607,7 +607,8 @@ int dh_set_params_ref(dh_handle* h, const float* ref, size_t count, void* stream
 
 int dh_set_gemm_mode(dh_handle* h, int mode) {
   if (!h) return fail(DH_EINVAL, "null handle");
-  if (mode != DH_GEMM_F32 && mode != DH_GEMM_X6 && mode != DH_GEMM_X6_ALL) return fail(DH_EINVAL, "bad GEMM mode");
+  if (mode != DH_GEMM_F32 && mode != DH_GEMM_X6 && mode != DH_GEMM_X6_ALL && mode != DH_GEMM_X6_ALL_UNFUSED)
+    return fail(DH_EINVAL, "bad GEMM mode");
   h->gemm_mode = mode;
   return DH_OK;
 }
@@ -637,7 +638,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // 24576 x 256 x 256 against 43 / 47 us for the exact-f32 gemm_ln_kernel;
   // tools/ln_gemm_bench.py on MI355X)
   const bool x6 = nt && gemm_x6_supported(D) &&
-                  (C > 1 ? h->gemm_mode != DH_GEMM_F32 : h->gemm_mode == DH_GEMM_X6_ALL);
+                  (C > 1 ? h->gemm_mode != DH_GEMM_F32
+                         : (h->gemm_mode == DH_GEMM_X6_ALL || h->gemm_mode == DH_GEMM_X6_ALL_UNFUSED));
   const bool ln_fused = nt && C == 1 && gemm_ln_supported(D, D);
   auto gemm = [&](const float* X, int ldx, const float* W, const float* Wt, const uint16_t* Wp, int ldw,
                   const float* bias, const float* Res, int ldr, float* Y, int ldy, int ncols, int K) {
@@ -665,6 +667,9 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // local energy, split-bf16, D = 256: the channel layer tail (Wo Wl + LN_ch, Wm + tanh_ch +
   // LN_ch) and the next linear map in ONE launch per layer (chain_ch_kernel)
   const bool chain_ch = C > 1 && x6 && nt && D == 256 && chain_ch_supported(d.N);
+  // local energy, split-bf16, D = 256, N <= 8: GEMM + channel LayerNorm fused per map
+  const bool lnch = C > 1 && x6 && !chain_ch && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&
+                    gemm_lnch_supported(d.N, D);
   {
     const bool wq = fold && !fused;
     if (!(geo_ready && h_feat && !wq)) {
@@ -725,6 +730,19 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
           launch_gemm_x6_ln(w.h, D, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
         else
           launch_gemm_ln(w.h, D, lp.WmT, D, lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
+      }
+      continue;
+    }
+    if (lnch) {
+      // channel rows: each linear map and its channel LayerNorm in one launch, in place over h
+      // (gemm_lnch.hip; the GEMM output never reaches HBM)
+      {
+        PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
+        launch_gemm_lnch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.geo, w.h, nw * d.N, 0, s);
+      }
+      {
+        PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
+        launch_gemm_lnch(d.N, w.h, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2, w.geo, w.h, nw * d.N, 1, s);
       }
       continue;
     }

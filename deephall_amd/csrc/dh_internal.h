@@ -114,6 +114,13 @@ struct X6Feat {
 };
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
+// gemm_lnch.hip: channel rows (C = 2N + 5 per electron, ne electrons), D = K = 256, N <= 8:
+// h = LN_ch(h + X W + b) (mode 0) or LN_ch(h + tanh_ch(h W + b)) (mode 1) in ONE launch,
+// in place over h [ne * C][256]; X [ne * C][256] (mode 1: X = h); split-bf16 arithmetic.
+// DH_LNCH=0 selects the GEMM + layernorm_ch pair instead.
+bool gemm_lnch_supported(int N, int D);
+void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
+                      const float* geo, float* h, int ne, int mode, hipStream_t s);
 bool chain_x6_enabled();
 bool chain_attn_supported(int N, int H, int dh);
 // Channel-row (C > 1) layer tail in one launch (gemm_x6.hip chain_ch_kernel; D = 256):

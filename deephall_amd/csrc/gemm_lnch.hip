@@ -1,0 +1,442 @@
+// Channel-row linear map + channel LayerNorm in ONE launch (local energy, D = K = 256):
+//
+//   MODE 0:  h = LN_ch(h + X W + b)            psiformer.py:44-46  (X = o, W = Wo Wl folded)
+//   MODE 1:  h = LN_ch(h + tanh_ch(h W + b))   psiformer.py:47-48  (X = h)
+//
+// in place over h [rows = ne * C][256], C = 2N + 5 channel rows per (walker, electron),
+// bias b on the value rows only; LN_ch / tanh_ch are layernorm.hip's channel rules.  It
+// replaces gemm_x6q (the GEMM writing t to HBM) + layernorm_ch_wave (reading t and h back):
+// the GEMM output never leaves the CU.
+//
+// Why a new tile shape.  The channel LayerNorm of one electron mixes its C rows feature by
+// feature (u_k = sum_t alpha_kt z_t, tanh_ch's sum_t z_t^2) and needs full-row sums over the
+// 256 features (means, z0 . z_c, |z_t|^2, |u_k|^2).  Here the MFMA column dimension is the
+// ELECTRON: a tile is 16 electrons x C channels (= 16 C rows, electron-aligned), and
+// wave w computes output features 32 w .. 32 w + 31 of all C channels of all 16 electrons.
+// With the weights as the MFMA A operand (v_mfma_f32_16x16x32_bf16: D col = lane & 15 =
+// electron, D row = 4 (lane >> 4) + reg = feature), lane (e, g) ends the k loop holding,
+// for electron e, features 32 w + 16 cb + 4 g .. +3 (cb = 0, 1) of EVERY channel row: the
+// channel algebra is lane-local, the feature sums are 8 lane-local values, a swap over
+// lanes e + 16 g (v_permlane16/32_swap) and one 8-wave LDS reduction per statistic.
+//
+// Split-bf16 arithmetic (gemm_x6.hip header): weights as pre-split planes Wp[3][ldp][K]
+// streamed L2 -> registers one k-step ahead (each wave uses only its own 32 feature columns,
+// so they need no LDS); the activation k-step (16 C rows x 32 k f32) is loaded by all 512
+// threads one step ahead into registers, split ONCE into three bf16 planes in LDS (every
+// element split by one thread; the MFMA loop reads the planes, no VALU split in it), two
+// plane buffers, one barrier per 32 k.  LDS plane image: [p][c][e][64 B], 16-B slot s of
+// electron e at s ^ f(e), f = {0, 2, 3, 1}[(e >> 2) & 3] (conflict-free ds_read_b128 for the
+// 16x16x32 lane groups, checked exhaustively).  Six MFMAs per product block, smallest
+// terms first (as gemm_x6m).
+//
+// Traffic per launch: X once (the k loop), h once (the epilogue; in MODE 1 the same rows
+// as X, from MALL), h written once: 12 * rows * 256 B, against 20 (MODE 0) / 24 (MODE 1)
+// for the two-kernel form.
+#include <cstdlib>
+
+#include "dh_internal.h"
+#include "device_common.h"
+
+namespace dh {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
+constexpr int LN_D = 256;   // features (= K)
+constexpr int LN_BK = 32;   // k per step
+
+__device__ __forceinline__ uint32_t pkbf(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
+}
+__device__ __forceinline__ float lo_of(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_of(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ int lnch_sw(int e) { return (0x78 >> (2 * ((e >> 2) & 3))) & 3; }
+
+// sum over the four lanes e, e + 16, e + 32, e + 48 (VALU swaps, every lane gets the sum)
+__device__ __forceinline__ float sum4g(float v) {
+  const int x = __float_as_int(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  v = __int_as_float(a[0]) + __int_as_float(a[1]);
+  const int y = __float_as_int(v);
+  const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);
+  return __int_as_float(b[0]) + __int_as_float(b[1]);
+}
+
+template <int N, int MODE, int NWV>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >= 8 ? 2 : 1, NWV >= 8 ? 2 : 1))) void gemm_lnch_kernel(const float* X, const uint16_t* __restrict__ Wp, int ldp,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ ln,
+                                                         const float* __restrict__ geo, float* h, int ne) {
+  constexpr int C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, K = LN_D, BK = LN_BK, NK = K / BK;
+  constexpr int ROWS = EPT * C;                    // activation rows per tile
+  constexpr int NT = NWV * 64, CB = D / (16 * NWV);  // threads; 16-column blocks per wave
+  constexpr int PLANE = C * EPT * 64;              // bytes of one bf16 plane per step
+  constexpr int STAGE = 3 * PLANE;
+  constexpr int NQ = (ROWS * 8 + NT - 1) / NT;     // 16-B activation pieces per thread per step
+  constexpr int NR = C + T + 3;                    // second-moment statistics per electron
+  constexpr int TS = NR | 1;                       // odd row stride of the totals
+  static_assert(2 * STAGE <= 163840, "LDS");
+  static_assert(NWV * NR * EPT * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
+  extern __shared__ float4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int tile = blockIdx.x;
+  const int e0 = tile * EPT;                       // first electron of the tile
+  const size_t row0 = (size_t)e0 * C;
+  const int rows_valid = min(ROWS, (ne - e0) * C);
+
+  // ---- activation pieces of this thread: piece i = tid + NT j -> (row i >> 3, quad i & 7)
+  int goff[NQ], loff[NQ];
+  bool gval[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int i = tid + NT * j;
+    const int r = i >> 3, q = i & 7;
+    gval[j] = i < ROWS * 8 && r < rows_valid;
+    const int e = r / C, c = r - e * C;
+    goff[j] = r * D + 4 * q;  // floats from row0 (k step added)
+    loff[j] = (c * EPT + e) * 64 + (((q >> 1) ^ lnch_sw(e)) * 16) + (q & 1) * 8;
+    if (!(i < ROWS * 8)) loff[j] = -1;
+  }
+  const float* Xt = X + row0 * D;
+  auto load_a = [&](int kt, float4 (&ra)[NQ]) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+      ra[j] = gval[j] ? *reinterpret_cast<const float4*>(Xt + goff[j] + kt * BK) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto split_store = [&](const float4 (&ra)[NQ], int buf) {
+    char* P = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      if (loff[j] < 0) continue;
+      const float4 u = ra[j];
+      const uint32_t h0 = pkbf(u.x, u.y), h1 = pkbf(u.z, u.w);
+      const float rx = u.x - lo_of(h0), ry = u.y - hi_of(h0), rz = u.z - lo_of(h1), rw = u.w - hi_of(h1);
+      const uint32_t m0 = pkbf(rx, ry), m1 = pkbf(rz, rw);
+      const uint32_t s0 = pkbf(rx - lo_of(m0), ry - hi_of(m0)), s1 = pkbf(rz - lo_of(m1), rw - hi_of(m1));
+      *reinterpret_cast<uint2*>(P + loff[j]) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(P + PLANE + loff[j]) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(P + 2 * PLANE + loff[j]) = make_uint2(s0, s1);
+    }
+  };
+  // ---- weight fragments of this wave: feature n = 16 (CB wid + cb) + l16, k = 32 kt + 8 kg
+  const uint16_t* wbase = Wp + (size_t)(16 * CB * wid + l16) * K + 8 * kg;
+  const size_t wplane = (size_t)ldp * K;
+  auto load_w = [&](int kt, int cb, bf16x8 (&wf)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      wf[p] = *reinterpret_cast<const bf16x8*>(wbase + p * wplane + (size_t)cb * 16 * K + kt * BK);
+  };
+  const int xoff = l16 * 64 + ((kg ^ lnch_sw(l16)) * 16);  // + c * EPT * 64 within a plane
+
+  f32x4 acc[C][CB];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  {
+    // column block outermost: one block's weight fragments (12 VGPRs) live at a time, the next
+    // block's streaming in behind them; the activation fragments are re-read from LDS per block
+    float4 ra[NQ];
+    bf16x8 wf[3], wn[3];
+    load_a(0, ra);
+    load_w(0, 0, wf);
+    split_store(ra, 0);
+    load_a(1, ra);
+#pragma unroll 1
+    for (int kt = 0; kt < NK; ++kt) {
+      __syncthreads();  // planes of step kt complete; step kt - 1's buffer is free
+      const char* P = smem + (kt & 1) * STAGE + xoff;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        // a compiler memory fence per block: the fragments are re-read, not kept live (CSE
+        // across blocks would hold all C channels' fragments in registers)
+        asm volatile("" ::: "memory");
+        if (cb + 1 < CB)
+          load_w(kt, cb + 1, wn);
+        else if (kt + 1 < NK)
+          load_w(kt + 1, 0, wn);
+        bf16x8 xf[2][3];
+        auto ldx = [&](int c, bf16x8 (&x)[3]) {
+          x[0] = *reinterpret_cast<const bf16x8*>(P + c * EPT * 64);
+          x[1] = *reinterpret_cast<const bf16x8*>(P + PLANE + c * EPT * 64);
+          x[2] = *reinterpret_cast<const bf16x8*>(P + 2 * PLANE + c * EPT * 64);
+        };
+        ldx(0, xf[0]);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          if (c + 1 < C) ldx(c + 1, xf[(c + 1) & 1]);  // one channel ahead
+          const bf16x8 x0 = xf[c & 1][0], x1 = xf[c & 1][1], x2 = xf[c & 1][2];
+          f32x4 a = acc[c][cb];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x2, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x0, a, 0, 0, 0);
+          acc[c][cb] = a;
+          if (cb == 0 && c == C / 2 && kt + 1 < NK) {
+            split_store(ra, (kt + 1) & 1);
+            if (kt + 2 < NK) load_a(kt + 2, ra);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wf[p] = wn[p];
+      }
+    }
+  }
+  __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
+
+  // ---- epilogue: lane = electron l16, features n0 + 16 cb + 4 kg + 0..3 of every channel row
+  const int E = e0 + l16;
+  const bool valid = E < ne;
+  const int b = (valid ? E : e0) / N;
+  const int nf = 16 * CB * wid + 4 * kg;  // + 16 cb
+  float* hr = h + ((size_t)(valid ? E : e0) * C) * D + nf;
+  float4 g[N];  // geometry of the walker's electrons (st, ct, sp, cp)
+#pragma unroll
+  for (int i = 0; i < N; ++i) g[i] = reinterpret_cast<const float4*>(geo)[(size_t)b * N + i];
+  auto al = [&](int k, int t) -> float {  // flow coefficient alpha_kt (layernorm.hip)
+    const float4 q = g[t >> 1];
+    if ((t & 1) == 0) return k == 0 ? -q.z : (k == 1 ? q.w : 0.f);
+    return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
+  };
+  // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[0][cb][0] += bv.x;
+    acc[0][cb][1] += bv.y;
+    acc[0][cb][2] += bv.z;
+    acc[0][cb][3] += bv.w;
+    if (MODE == 1) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float z0 = acc[0][cb][v];
+        const float y0 = tanhf(z0), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
+        float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const float zt = acc[1 + t][cb][v];
+          sq = fmaf(zt, zt, sq);
+          u0 = fmaf(al(0, t), zt, u0);
+          u1 = fmaf(al(1, t), zt, u1);
+          u2 = fmaf(al(2, t), zt, u2);
+          acc[1 + t][cb][v] = d1 * zt;
+        }
+        acc[0][cb][v] = y0;
+        acc[1 + T][cb][v] = d1 * acc[1 + T][cb][v] + d2 * sq;
+        acc[2 + T][cb][v] = d1 * acc[2 + T][cb][v] + d2 * (u0 * u0);
+        acc[3 + T][cb][v] = d1 * acc[3 + T][cb][v] + d2 * (u1 * u1);
+        acc[4 + T][cb][v] = d1 * acc[4 + T][cb][v] + d2 * (u2 * u2);
+      }
+    }
+  }
+  {
+    // residual rows, PF float4 loads in flight (sched barriers keep the compiler from
+    // hoisting all C * CB of them, which would spill the accumulators)
+    constexpr int NRES = C * CB, PF = 8;
+    float4 rb[PF];
+    auto rp = [&](int i) { return reinterpret_cast<const float4*>(hr + (size_t)(i / CB) * D + 16 * (i % CB)); };
+#pragma unroll
+    for (int i = 0; i < PF && i < NRES; ++i) rb[i] = *rp(i);
+#pragma unroll
+    for (int i = 0; i < NRES; ++i) {
+      const float4 r = rb[i % PF];
+      if (i + PF < NRES) rb[i % PF] = *rp(i + PF);
+      f32x4& a = acc[i / CB][i % CB];
+      a[0] = r.x + a[0];
+      a[1] = r.y + a[1];
+      a[2] = r.z + a[2];
+      a[3] = r.w + a[3];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float* red = reinterpret_cast<float*>(smem);   // [NWV waves][NR][EPT] partial sums
+  float* tot = red + NWV * NR * EPT;              // [EPT][TS] totals (odd stride: 16 banks)
+  auto lane_sum = [&](int c) {
+    float r = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) r += (acc[c][cb][0] + acc[c][cb][1]) + (acc[c][cb][2] + acc[c][cb][3]);
+    return r;
+  };
+  // reduce NS per-lane partials part(j) over the tile's 256 features -> mean in tot[e][j]
+  auto reduce = [&](auto part, auto NS_) {
+    constexpr int NS = decltype(NS_)::value;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const float v = sum4g(part(j));
+      if (kg == 0) red[(wid * NS + j) * EPT + l16] = v;
+      __builtin_amdgcn_sched_barrier(0);  // one statistic at a time (register pressure)
+    }
+    __syncthreads();
+    for (int i = tid; i < NS * EPT; i += NT) {
+      const int j = i / EPT, e = i - j * EPT;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) s += red[(w * NS + j) * EPT + e];
+      tot[e * TS + j] = s * (1.f / D);
+    }
+    __syncthreads();
+  };
+  const float* mt = tot + l16 * TS;  // this lane's electron
+  // channel means, centre
+  reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float mu = mt[c];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[c][cb][v] -= mu;
+  }
+  // flow vector u_k = sum_t alpha_kt z_t of columns block cb (recomputed where needed)
+  auto flow = [&](int k, int cb) {
+    f32x4 r = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (k == 2 && (t & 1) == 0) continue;  // alpha_2,2i = 0
+      const float a = al(k, t);
+      r[0] = fmaf(a, acc[1 + t][cb][0], r[0]);
+      r[1] = fmaf(a, acc[1 + t][cb][1], r[1]);
+      r[2] = fmaf(a, acc[1 + t][cb][2], r[2]);
+      r[3] = fmaf(a, acc[1 + t][cb][3], r[3]);
+    }
+    return r;
+  };
+  auto dot4 = [](const f32x4& x, const f32x4& y) { return (x[0] * y[0] + x[1] * y[1]) + (x[2] * y[2] + x[3] * y[3]); };
+  // p_c = <z0 z_c>, q_t = <z_t^2>, uu_k = <u_k^2>
+  reduce(
+      [&](int j) {
+        float r = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          if (j < C) {
+            r += dot4(acc[0][cb], acc[j][cb]);
+          } else if (j < C + T) {
+            r += dot4(acc[1 + j - C][cb], acc[1 + j - C][cb]);
+          } else {
+            const f32x4 u = flow(j - C - T, cb);
+            r += dot4(u, u);
+          }
+        }
+        return r;
+      },
+      std::integral_constant<int, NR>{});
+  const float s = 1.f / sqrtf(mt[0] + 1e-5f), s2 = s * s;
+  float cl = 0.f, au[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const float a = s2 * mt[1 + t];
+    cl += 3.f * a * a - s2 * mt[C + t];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) au[k] = fmaf(al(k, t), a, au[k]);
+  }
+  float cs[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cs[k] = 3.f * au[k] * au[k] - s2 * mt[C + T + k];
+  const float aL = s2 * mt[1 + T];
+  if (!valid) return;
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const float4 gv = *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
+    const float4 bb = *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb);
+    const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bq[4] = {bb.x, bb.y, bb.z, bb.w};
+    float gs[4], z0[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      gs[v] = gg[v] * s;
+      z0[v] = acc[0][cb][v];
+    }
+    float* o = hr + 16 * cb;
+    *reinterpret_cast<float4*>(o) = make_float4(gg[0] * (s * z0[0]) + bq[0], gg[1] * (s * z0[1]) + bq[1],
+                                                gg[2] * (s * z0[2]) + bq[2], gg[3] * (s * z0[3]) + bq[3]);
+    float sat[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float at = s2 * mt[1 + t];
+      float y[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float zt = acc[1 + t][cb][v];
+        sat[v] = fmaf(at, zt, sat[v]);
+        y[v] = gs[v] * (zt - at * z0[v]);
+      }
+      *reinterpret_cast<float4*>(o + (size_t)(1 + t) * D) = make_float4(y[0], y[1], y[2], y[3]);
+    }
+    {
+      float y[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) y[v] = gs[v] * (acc[1 + T][cb][v] - aL * z0[v] - 2.f * sat[v] + cl * z0[v]);
+      *reinterpret_cast<float4*>(o + (size_t)(1 + T) * D) = make_float4(y[0], y[1], y[2], y[3]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const f32x4 uk = flow(k, cb);
+      const float ak = s2 * mt[2 + T + k];
+      float y[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        y[v] = gs[v] * (acc[2 + T + k][cb][v] - ak * z0[v] - 2.f * au[k] * uk[v] + cs[k] * z0[v]);
+      *reinterpret_cast<float4*>(o + (size_t)(2 + T + k) * D) = make_float4(y[0], y[1], y[2], y[3]);
+    }
+  }
+}
+
+template <int N, int NWV>
+void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
+                   float* h, int ne, int mode, hipStream_t s) {
+  constexpr int C = 2 * N + 5;
+  const size_t smem = 2ull * 3 * C * LN_EPT * 64;
+  const int grid = (ne + LN_EPT - 1) / LN_EPT;
+  if (mode == 0) {
+    ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);
+    hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
+                       ne);
+  } else {
+    ensure_smem(gemm_lnch_kernel<N, 1, NWV>, smem);
+    hipLaunchKernelGGL((gemm_lnch_kernel<N, 1, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
+                       ne);
+  }
+}
+
+template <int N>
+void launch_lnch_n(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
+                   float* h, int ne, int mode, hipStream_t s) {
+  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s);
+}
+
+}  // namespace
+
+bool gemm_lnch_supported(int N, int D) {
+  if (D != LN_D || N < 1 || N > 6) return false;
+  static int env = -1;
+  if (env < 0) {
+    const char* v = getenv("DH_LNCH");
+    env = (v && v[0] == '0') ? 0 : 1;
+  }
+  return env != 0;
+}
+
+void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
+                      const float* geo, float* h, int ne, int mode, hipStream_t s) {
+  switch (N) {
+    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+  }
+}
+
+}  // namespace dh

@@ -110,7 +110,8 @@ class NativeHandle:
 
     def set_gemm_mode(self, mode: str):
         """GEMM arithmetic: "x6all" (split-bf16, f32-accurate, every GEMM; default), "x6"
-        (split-bf16 for the local-energy channel rows only) or "f32" (exact-f32 MFMA)."""
+        (split-bf16 for the local-energy channel rows only), "f32" (exact-f32 MFMA) or
+        "x6all_unfused" (as x6all with the channel LayerNorms as separate passes; test hook)."""
         _lib.check(self.lib.dh_set_gemm_mode(self.h, _GEMM_MODES[mode]))
 
     def __del__(self):
@@ -142,7 +143,7 @@ class NativeHandle:
         self._params_key = key
 
 
-_GEMM_MODES = {"f32": 0, "x6": 1, "x6all": 2}
+_GEMM_MODES = {"f32": 0, "x6": 1, "x6all": 2, "x6all_unfused": 3}
 _GEMM_MODE = os.environ.get("DH_GEMM", "x6all")
 if _GEMM_MODE not in _GEMM_MODES:
     raise ValueError(f"DH_GEMM must be one of {sorted(_GEMM_MODES)}, got {_GEMM_MODE!r}")

@@ -190,10 +190,14 @@ int dh_adam_update(float* params, const float* grad, float* mu, float* nu, size_
  *                 f32 matrix rate.
  *   DH_GEMM_X6_ALL  split-bf16 also for the log-psi / MCMC GEMMs (the two per layer that
  *                 carry a LayerNorm with it in their epilogue).  Default.
+ *   DH_GEMM_X6_ALL_UNFUSED  as DH_GEMM_X6_ALL, but the local energy's channel LayerNorms run
+ *                 as separate passes after their GEMMs instead of inside them (test hook for
+ *                 the fused gemm_lnch kernel; same arithmetic up to f32 summation order).
  * In DH_GEMM_F32 and DH_GEMM_X6 the log-psi / MCMC passes use the exact-f32 kernels. */
 #define DH_GEMM_F32 0
 #define DH_GEMM_X6 1
 #define DH_GEMM_X6_ALL 2
+#define DH_GEMM_X6_ALL_UNFUSED 3
 int dh_set_gemm_mode(dh_handle* h, int mode);
 
 /* Workspace bytes needed to process `batch` walkers: op 0 = log psi / MCMC,

@@ -1,0 +1,71 @@
+"""The fused channel GEMM + LayerNorm kernel (gemm_lnch.hip) against the two-pass form.
+
+Round 3 moved each channel-row linear map of the local energy and the channel LayerNorm
+after it (psiformer.py:44-48: h = LN(h + o Wo Wl + b), h = LN(h + tanh(h Wm + b))) into
+ONE launch.  The two-pass form (split-bf16 GEMM writing t, then layernorm_ch reading it)
+stays reachable as the GEMM mode "x6all_unfused".  Both compute the same f32 arithmetic up
+to summation order, so every observable must agree to f32 rounding on every walker
+(relative, floor 1): median <= 5e-6, worst <= 1e-3 (an ill-conditioned orbital matrix
+amplifies rounding-level differences, as in the f32-floor fixtures).  Parity of the fused
+path against the float64 oracle is tests/test_gpu_floor.py and tests/test_gpu_parity.py,
+which run in the default (fused) mode.
+
+Cases: N = 1, 2, 3 (C1), 5 (mixed spins), 6 (C2); batches whose electron count is not a
+multiple of the 16-electron tile (a partial last tile); C2 at the bench batch (4096).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from deephall_amd import hamiltonian
+from deephall_amd.networks import psiformer as PF
+from helpers import make_params, make_walkers, to_device_params
+from oracle import reference as R
+from test_gpu_parity import build
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("N1", dict(nspins=(1, 0), flux=2), 7),
+    ("N2", dict(nspins=(2, 0), flux=3), 13),
+    ("C1", dict(nspins=(3, 0), flux=2), 37),
+    ("N5mix", dict(nspins=(3, 2), flux=6), 21),
+    ("C2", dict(nspins=(6, 0), flux=15), 43),
+    ("C2_bench", dict(nspins=(6, 0), flux=15), 4096),
+]
+OBS = ["kinetic", "potential", "angular_momentum_z", "angular_momentum_z_square", "angular_momentum_square"]
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return np.abs(a - b) / np.maximum(np.abs(b), 1.0)
+
+
+def run(model, system, params, x, mode):
+    PF.set_gemm_mode(mode)
+    try:
+        e, o = hamiltonian.local_energy(model, system)(params, x)
+        torch.cuda.synchronize()
+        return {"e_l": e.cpu().numpy(), **{k: o[k].cpu().numpy() for k in OBS}}
+    finally:
+        PF.set_gemm_mode("x6all")
+
+
+@pytest.mark.parametrize("tag,kw,B", CASES, ids=[c[0] for c in CASES])
+def test_fused_matches_two_pass(cuda, tag, kw, B):
+    ocfg = R.OracleConfig(**kw)
+    system, model = build(ocfg)
+    params = to_device_params(make_params(ocfg, seed=11))
+    N = sum(kw["nspins"])
+    x = torch.tensor(make_walkers(B, N, seed=5 + B), device=cuda)
+    fused = run(model, system, params, x, "x6all")
+    split = run(model, system, params, x, "x6all_unfused")
+    for k in fused:
+        assert np.all(np.isfinite(fused[k])), (tag, k)
+        err = rel(fused[k], split[k])
+        print(f"{tag} {k}: max {err.max():.2e} median {np.median(err):.2e}")
+        assert np.median(err) <= 5e-6, (tag, k, np.median(err))
+        assert err.max() <= 1e-3, (tag, k, err.max())
