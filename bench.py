@@ -241,8 +241,8 @@ def main():
         traffic = tj.get("channel_gemm_bytes_per_launch") if x6 else None
         traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})" if traffic else None
     # dominant kernel: the local-energy channel GEMM (class gemm_ch of dh_profile_read; in
-    # the split-bf16 modes gemm_x6m_kernel for the wide maps and gemm_x6q_kernel for the
-    # 256-column ones, ~33 % of the step).  Its arithmetic
+    # the split-bf16 modes gemm_x6m_kernel for the wide maps and gemm_lnch_kernel, GEMM +
+    # channel LayerNorm, for the 256-column ones).  Its arithmetic
     # runs as 6 bf16 MFMA products per f32 product, so the ceiling of its algorithmic f32
     # flop rate is the dense bf16 MFMA peak / 6.  The log-psi GEMMs (class gemm: exact-f32
     # gemm_ln_kernel + split-bf16 gemm_x6d_kernel) are reported beside it.
@@ -255,9 +255,10 @@ def main():
     achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
     peak = PEAK_BF16_MFMA_TFLOPS / 6 if x6 else PEAK_F32_MFMA_TFLOPS
     roofline = {
-        "kernel": ("local-energy channel GEMMs, persistent split-bf16 f32 GEMM: gemm_x6m_kernel "
-                   "(v_mfma_f32_16x16x32_bf16; q|k|v and orbital maps) + gemm_x6q_kernel "
-                   "(v_mfma_f32_32x32x16_bf16; the 256-column maps), averaged over the 6 launches"
+        "kernel": ("local-energy channel GEMMs, split-bf16 f32 GEMM (v_mfma_f32_16x16x32_bf16): "
+                   "gemm_x6m_kernel (q|k|v and orbital maps) + gemm_lnch_kernel (the 256-column maps "
+                   "with the channel LayerNorm fused in; its LN work counted in the launch time, not "
+                   "in the flops), averaged over the 6 launches"
                    if x6 else "gemm_ntp_kernel (exact-f32 channel GEMMs)"),
         "bound": "mfma",
         "achieved": round(achieved, 2),

@@ -16,8 +16,8 @@
 // With the weights as the MFMA A operand (v_mfma_f32_16x16x32_bf16: D col = lane & 15 =
 // electron, D row = 4 (lane >> 4) + reg = feature), lane (e, g) ends the k loop holding,
 // for electron e, features 32 w + 16 cb + 4 g .. +3 (cb = 0, 1) of EVERY channel row: the
-// channel algebra is lane-local, the feature sums are 8 lane-local values, a swap over
-// lanes e + 16 g (v_permlane16/32_swap) and one 8-wave LDS reduction per statistic.
+// channel algebra is lane-local, the feature sums are 8 lane-local values and one LDS
+// reduction over the 32 lanes (8 waves x 4 lane rows) holding that electron.
 //
 // Split-bf16 arithmetic (gemm_x6.hip header): weights as pre-split planes Wp[3][ldp][K]
 // streamed L2 -> registers one k-step ahead (each wave uses only its own 32 feature columns,
@@ -37,6 +37,10 @@
 #include "dh_internal.h"
 #include "device_common.h"
 
+#ifndef LNCH_OPQ
+#define LNCH_OPQ 1
+#endif
+
 namespace dh {
 
 namespace {
@@ -45,6 +49,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
 constexpr int LN_D = 256;   // features (= K)
@@ -56,16 +61,6 @@ __device__ __forceinline__ uint32_t pkbf(float x, float y) {
 __device__ __forceinline__ float lo_of(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_of(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ int lnch_sw(int e) { return (0x78 >> (2 * ((e >> 2) & 3))) & 3; }
-
-// sum over the four lanes e, e + 16, e + 32, e + 48 (VALU swaps, every lane gets the sum)
-__device__ __forceinline__ float sum4g(float v) {
-  const int x = __float_as_int(v);
-  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  v = __int_as_float(a[0]) + __int_as_float(a[1]);
-  const int y = __float_as_int(v);
-  const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);
-  return __int_as_float(b[0]) + __int_as_float(b[1]);
-}
 
 template <int N, int MODE, int NWV>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >= 8 ? 2 : 1, NWV >= 8 ? 2 : 1))) void gemm_lnch_kernel(const float* X, const uint16_t* __restrict__ Wp, int ldp,
@@ -81,7 +76,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   constexpr int NR = C + T + 3;                    // second-moment statistics per electron
   constexpr int TS = NR | 1;                       // odd row stride of the totals
   static_assert(2 * STAGE <= 163840, "LDS");
-  static_assert(NWV * NR * EPT * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
+  static_assert(NWV * NR * 64 * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -93,23 +88,24 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const int rows_valid = min(ROWS, (ne - e0) * C);
 
   // ---- activation pieces of this thread: piece i = tid + NT j -> (row i >> 3, quad i & 7)
+  // buffer descriptor over the tile's activation rows (tile-uniform base; rows past the last
+  // electron are out of range: their loads return 0)
+  const uint32_t tbytes = (uint32_t)rows_valid * D * 4;
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X) + row0 * D, (short)0, tbytes, 0x00020000);
   int goff[NQ], loff[NQ];
-  bool gval[NQ];
 #pragma unroll
   for (int j = 0; j < NQ; ++j) {
     const int i = tid + NT * j;
     const int r = i >> 3, q = i & 7;
-    gval[j] = i < ROWS * 8 && r < rows_valid;
     const int e = r / C, c = r - e * C;
-    goff[j] = r * D + 4 * q;  // floats from row0 (k step added)
+    goff[j] = i < ROWS * 8 ? (r * D + 4 * q) * 4 : 0x7fffffff;  // bytes from row0 (k step in soffset)
     loff[j] = (c * EPT + e) * 64 + (((q >> 1) ^ lnch_sw(e)) * 16) + (q & 1) * 8;
     if (!(i < ROWS * 8)) loff[j] = -1;
   }
-  const float* Xt = X + row0 * D;
   auto load_a = [&](int kt, float4 (&ra)[NQ]) {
 #pragma unroll
     for (int j = 0; j < NQ; ++j)
-      ra[j] = gval[j] ? *reinterpret_cast<const float4*>(Xt + goff[j] + kt * BK) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsX, goff[j], kt * BK * 4, 0));
   };
   auto split_store = [&](const float4 (&ra)[NQ], int buf) {
     char* P = smem + buf * STAGE;
@@ -201,7 +197,19 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const bool valid = E < ne;
   const int b = (valid ? E : e0) / N;
   const int nf = 16 * CB * wid + 4 * kg;  // + 16 cb
-  float* hr = h + ((size_t)(valid ? E : e0) * C) * D + nf;
+  // this lane's rows of h (invalid electrons read the tile's first rows and store nothing);
+  // row addresses pass through an opaque asm so the compiler forms them one at a time
+  // (precomputing all 2 C of them spills)
+  float* const hrow = h + (row0 + (size_t)(valid ? l16 : 0) * C) * D + nf;
+  auto rowp = [&](int c) {
+    float* p = hrow + c * D;
+    asm volatile("" : "+v"(p));
+    return p;
+  };
+  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(rowp(c) + 16 * cb); };
+  auto sth = [&](int c, int cb, float4 v) {
+    if (valid) *reinterpret_cast<float4*>(rowp(c) + 16 * cb) = v;
+  };
   float4 g[N];  // geometry of the walker's electrons (st, ct, sp, cp)
 #pragma unroll
   for (int i = 0; i < N; ++i) g[i] = reinterpret_cast<const float4*>(geo)[(size_t)b * N + i];
@@ -238,31 +246,33 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         acc[2 + T][cb][v] = d1 * acc[2 + T][cb][v] + d2 * (u0 * u0);
         acc[3 + T][cb][v] = d1 * acc[3 + T][cb][v] + d2 * (u1 * u1);
         acc[4 + T][cb][v] = d1 * acc[4 + T][cb][v] + d2 * (u2 * u2);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
   {
-    // residual rows, PF float4 loads in flight (sched barriers keep the compiler from
+    // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
     // hoisting all C * CB of them, which would spill the accumulators)
     constexpr int NRES = C * CB, PF = 8;
     float4 rb[PF];
-    auto rp = [&](int i) { return reinterpret_cast<const float4*>(hr + (size_t)(i / CB) * D + 16 * (i % CB)); };
 #pragma unroll
-    for (int i = 0; i < PF && i < NRES; ++i) rb[i] = *rp(i);
+    for (int i = 0; i < PF && i < NRES; ++i) rb[i] = ldh(i / CB, i % CB);
 #pragma unroll
     for (int i = 0; i < NRES; ++i) {
       const float4 r = rb[i % PF];
-      if (i + PF < NRES) rb[i % PF] = *rp(i + PF);
+      if (i + PF < NRES) rb[i % PF] = ldh((i + PF) / CB, (i + PF) % CB);
       f32x4& a = acc[i / CB][i % CB];
       a[0] = r.x + a[0];
       a[1] = r.y + a[1];
       a[2] = r.z + a[2];
       a[3] = r.w + a[3];
-      __builtin_amdgcn_sched_barrier(0);
+#if LNCH_OPQ
+      asm volatile("" : "+v"(a));  // consumed here, before the next load is issued
+#endif
     }
   }
-  float* red = reinterpret_cast<float*>(smem);   // [NWV waves][NR][EPT] partial sums
-  float* tot = red + NWV * NR * EPT;              // [EPT][TS] totals (odd stride: 16 banks)
+  float* red = reinterpret_cast<float*>(smem);   // [NWV waves][NR][64 lanes] partial sums
+  float* tot = red + NWV * NR * 64;               // [EPT][TS] totals (odd stride: 16 banks)
   auto lane_sum = [&](int c) {
     float r = 0.f;
 #pragma unroll
@@ -274,16 +284,17 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     constexpr int NS = decltype(NS_)::value;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      const float v = sum4g(part(j));
-      if (kg == 0) red[(wid * NS + j) * EPT + l16] = v;
-      __builtin_amdgcn_sched_barrier(0);  // one statistic at a time (register pressure)
+      red[(wid * NS + j) * 64 + lane] = part(j);  // every lane's 8-feature partial (no cross-lane ops)
+      __builtin_amdgcn_sched_barrier(0);          // one statistic at a time (register pressure)
     }
     __syncthreads();
     for (int i = tid; i < NS * EPT; i += NT) {
       const int j = i / EPT, e = i - j * EPT;
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < NWV; ++w) s += red[(w * NS + j) * EPT + e];
+      for (int w = 0; w < NWV; ++w)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
       tot[e * TS + j] = s * (1.f / D);
     }
     __syncthreads();
@@ -298,6 +309,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) acc[c][cb][v] -= mu;
+    __builtin_amdgcn_sched_barrier(0);
   }
   // flow vector u_k = sum_t alpha_kt z_t of columns block cb (recomputed where needed)
   auto flow = [&](int k, int cb) {
@@ -345,7 +357,6 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
   for (int k = 0; k < 3; ++k) cs[k] = 3.f * au[k] * au[k] - s2 * mt[C + T + k];
   const float aL = s2 * mt[1 + T];
-  if (!valid) return;
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
     const float4 gv = *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
@@ -357,9 +368,8 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       gs[v] = gg[v] * s;
       z0[v] = acc[0][cb][v];
     }
-    float* o = hr + 16 * cb;
-    *reinterpret_cast<float4*>(o) = make_float4(gg[0] * (s * z0[0]) + bq[0], gg[1] * (s * z0[1]) + bq[1],
-                                                gg[2] * (s * z0[2]) + bq[2], gg[3] * (s * z0[3]) + bq[3]);
+    sth(0, cb, make_float4(gg[0] * (s * z0[0]) + bq[0], gg[1] * (s * z0[1]) + bq[1], gg[2] * (s * z0[2]) + bq[2],
+                           gg[3] * (s * z0[3]) + bq[3]));
     float sat[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -371,13 +381,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         sat[v] = fmaf(at, zt, sat[v]);
         y[v] = gs[v] * (zt - at * z0[v]);
       }
-      *reinterpret_cast<float4*>(o + (size_t)(1 + t) * D) = make_float4(y[0], y[1], y[2], y[3]);
+      sth(1 + t, cb, make_float4(y[0], y[1], y[2], y[3]));
+      __builtin_amdgcn_sched_barrier(0);
     }
     {
       float y[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) y[v] = gs[v] * (acc[1 + T][cb][v] - aL * z0[v] - 2.f * sat[v] + cl * z0[v]);
-      *reinterpret_cast<float4*>(o + (size_t)(1 + T) * D) = make_float4(y[0], y[1], y[2], y[3]);
+      sth(1 + T, cb, make_float4(y[0], y[1], y[2], y[3]));
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -387,7 +398,8 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
       for (int v = 0; v < 4; ++v)
         y[v] = gs[v] * (acc[2 + T + k][cb][v] - ak * z0[v] - 2.f * au[k] * uk[v] + cs[k] * z0[v]);
-      *reinterpret_cast<float4*>(o + (size_t)(2 + T + k) * D) = make_float4(y[0], y[1], y[2], y[3]);
+      sth(2 + T + k, cb, make_float4(y[0], y[1], y[2], y[3]));
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }

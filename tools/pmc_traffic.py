@@ -37,8 +37,9 @@ def main(paths):
         tot_b += (rd + wr) * nf
         tot_n += nf
     out["gemm_bytes_per_launch"] = tot_b / tot_n if tot_n else None
-    # the local-energy channel GEMMs alone (persistent split-bf16 kernel families)
-    ch = [v for k, v in out["kernels"].items() if k.startswith(("gemm_x6q_kernel", "gemm_x6m_kernel"))]
+    # the local-energy channel GEMMs alone (split-bf16 kernel families, incl. the fused
+    # GEMM + channel LayerNorm of gemm_lnch.hip)
+    ch = [v for k, v in out["kernels"].items() if k.startswith(("gemm_x6q_kernel", "gemm_x6m_kernel", "gemm_lnch_kernel"))]
     n_ch = sum(v["launches"] for v in ch)
     out["channel_gemm_bytes_per_launch"] = (
         sum(v["bytes_per_launch"] * v["launches"] for v in ch) / n_ch if n_ch else None)
