@@ -1546,6 +1546,15 @@ int dh_debug_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const floa
   return check_launch();
 }
 
+int dh_debug_gemm_lnch(int N, int mode, const float* X, const uint16_t* Wp, int ldp, const float* bias,
+                       const float* ln, const float* geo, float* h, int ne, void* stream) {
+  if (!gemm_lnch_supported(N, 256) || (mode != 0 && mode != 1) || (mode == 0 && !X) || !Wp || !ln || !geo || !h ||
+      ne < 1 || ldp < x6_plane_rows(256) || ne % N)
+    return fail(DH_EINVAL, "bad gemm_lnch args");
+  launch_gemm_lnch(N, mode == 0 ? X : h, Wp, ldp, bias, ln, geo, h, ne, mode, (hipStream_t)stream);
+  return check_launch();
+}
+
 int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
                      const float* ln, float* h, int rows, int K, void* stream) {
   if (!gemm_ln_supported(256, K) || rows < 1 || (mode != 0 && mode != 1)) return fail(DH_EINVAL, "bad gemm_ln args");

@@ -37,6 +37,12 @@
 #include "dh_internal.h"
 #include "device_common.h"
 
+#ifndef LNCH_PF
+#define LNCH_PF 8
+#endif
+#ifndef LNCH_ABL
+#define LNCH_ABL 0
+#endif
 #ifndef LNCH_OPQ
 #define LNCH_OPQ 1
 #endif
@@ -75,7 +81,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   constexpr int NQ = (ROWS * 8 + NT - 1) / NT;     // 16-B activation pieces per thread per step
   constexpr int NR = C + T + 3;                    // second-moment statistics per electron
   constexpr int TS = NR | 1;                       // odd row stride of the totals
-  static_assert(2 * STAGE <= 163840, "LDS");
+  static_assert(2 * STAGE + ((EPT + N - 1) / N + 1) * N * 16 <= 163840, "LDS");
   static_assert(NWV * NR * 64 * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
@@ -87,6 +93,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const size_t row0 = (size_t)e0 * C;
   const int rows_valid = min(ROWS, (ne - e0) * C);
 
+  // geometry of the walkers the tile's electrons belong to, staged once in LDS past the
+  // stage buffers (visible after the k loop's barriers)
+  constexpr int GW = (EPT + N - 1) / N + 1;  // walkers a 16-electron tile can touch
+  float4* gl = reinterpret_cast<float4*>(smem + 2 * STAGE);
+  if (tid < GW * N) {
+    const int ge = (e0 / N) * N + tid;
+    gl[tid] = ge < ne ? reinterpret_cast<const float4*>(geo)[ge] : make_float4(0.f, 1.f, 0.f, 1.f);
+  }
   // ---- activation pieces of this thread: piece i = tid + NT j -> (row i >> 3, quad i & 7)
   // buffer descriptor over the tile's activation rows (tile-uniform base; rows past the last
   // electron are out of range: their loads return 0)
@@ -132,11 +146,50 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   };
   const int xoff = l16 * 64 + ((kg ^ lnch_sw(l16)) * 16);  // + c * EPT * 64 within a plane
 
+  // lane = electron l16 of the tile; its accumulators hold features nf + 16 cb + 0..3 of every
+  // channel row (MFMA D layout: col = lane & 15, row = 4 (lane >> 4) + reg)
+  const int E = e0 + l16;
+  const bool valid = E < ne;
+  const int b = (valid ? E : e0) / N;
+  const int nf = 16 * CB * wid + 4 * kg;  // + 16 cb
+  // this lane's rows of h (invalid electrons read the tile's first rows and store nothing);
+  // 32-bit offsets from the tile's base, each passed through an opaque asm so the compiler
+  // forms them one at a time (precomputing all 2 C row addresses spills)
+  char* const htile = reinterpret_cast<char*>(h + row0 * D);  // tile-uniform base (SGPRs)
+  const uint32_t hv = (uint32_t)(((valid ? l16 : 0) * C * D + nf) * 4);
+  auto roff = [&](int c, int cb) {  // 32-bit byte offset of (row c, block cb): saddr + voffset
+    uint32_t o = hv + (uint32_t)((c * D + 16 * cb) * 4);
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(htile + roff(c, cb)); };
+  auto sth = [&](int c, int cb, float4 v) {
+    if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
+  };
+  // MODE 0: the accumulators start from the residual h (+ the bias on the value rows), loaded
+  // here with the first activation loads, so the epilogue has no residual round trips
   f32x4 acc[C][CB];
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int cb = 0; cb < CB; ++cb) {
+      if (MODE == 0) {
+        const float4 r = ldh(c, cb);
+        acc[c][cb] = (f32x4){r.x, r.y, r.z, r.w};
+      } else {
+        acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  if (MODE == 0 && bias) {
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const float4 bv = *reinterpret_cast<const float4*>(bias + nf + 16 * cb);
+      acc[0][cb][0] += bv.x;
+      acc[0][cb][1] += bv.y;
+      acc[0][cb][2] += bv.z;
+      acc[0][cb][3] += bv.w;
+    }
+  }
 
   {
     // column block outermost: one block's weight fragments (12 VGPRs) live at a time, the next
@@ -172,6 +225,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           if (c + 1 < C) ldx(c + 1, xf[(c + 1) & 1]);  // one channel ahead
           const bf16x8 x0 = xf[c & 1][0], x1 = xf[c & 1][1], x2 = xf[c & 1][2];
           f32x4 a = acc[c][cb];
+#if LNCH_ABL & 2
+          if (a[0] == 1.2345e-33f)  // ablation (tools only): MFMAs skipped
+#endif
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x2, a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], x0, a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x1, a, 0, 0, 0);
@@ -191,42 +247,36 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     }
   }
   __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
+#if LNCH_ABL & 1
+  {  // ablation (tools only): no LayerNorm epilogue, the raw accumulators stored
+    const int E = e0 + l16;
+    if (E < ne) {
+      float* hr = h + (row0 + (size_t)l16 * C) * D + 16 * CB * wid + 4 * kg;
+      for (int c = 0; c < C; ++c)
+        for (int cb = 0; cb < CB; ++cb) *reinterpret_cast<f32x4*>(hr + c * D + 16 * cb) = acc[c][cb];
+    }
+    return;
+  }
+#endif
 
-  // ---- epilogue: lane = electron l16, features n0 + 16 cb + 4 kg + 0..3 of every channel row
-  const int E = e0 + l16;
-  const bool valid = E < ne;
-  const int b = (valid ? E : e0) / N;
-  const int nf = 16 * CB * wid + 4 * kg;  // + 16 cb
-  // this lane's rows of h (invalid electrons read the tile's first rows and store nothing);
-  // row addresses pass through an opaque asm so the compiler forms them one at a time
-  // (precomputing all 2 C of them spills)
-  float* const hrow = h + (row0 + (size_t)(valid ? l16 : 0) * C) * D + nf;
-  auto rowp = [&](int c) {
-    float* p = hrow + c * D;
-    asm volatile("" : "+v"(p));
-    return p;
-  };
-  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(rowp(c) + 16 * cb); };
-  auto sth = [&](int c, int cb, float4 v) {
-    if (valid) *reinterpret_cast<float4*>(rowp(c) + 16 * cb) = v;
-  };
-  float4 g[N];  // geometry of the walker's electrons (st, ct, sp, cp)
-#pragma unroll
-  for (int i = 0; i < N; ++i) g[i] = reinterpret_cast<const float4*>(geo)[(size_t)b * N + i];
+  // ---- epilogue: lane = electron l16, features nf + 16 cb + 0..3 of every channel row
+  // geometry of the walker's electrons (st, ct, sp, cp) from the tile's LDS copy (read where
+  // used: holding N float4 per lane would spill the accumulators)
+  const float4* gw = gl + (b - e0 / N) * N;
   auto al = [&](int k, int t) -> float {  // flow coefficient alpha_kt (layernorm.hip)
-    const float4 q = g[t >> 1];
+    const float4 q = gw[t >> 1];
     if ((t & 1) == 0) return k == 0 ? -q.z : (k == 1 ? q.w : 0.f);
     return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
   };
-  // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
+  // pre-LN rows x_c (in acc; MODE 0: complete): MODE 1's bias (value rows), tanh_ch, then + h
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
-    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-    acc[0][cb][0] += bv.x;
-    acc[0][cb][1] += bv.y;
-    acc[0][cb][2] += bv.z;
-    acc[0][cb][3] += bv.w;
     if (MODE == 1) {
+      const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[0][cb][0] += bv.x;
+      acc[0][cb][1] += bv.y;
+      acc[0][cb][2] += bv.z;
+      acc[0][cb][3] += bv.w;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float z0 = acc[0][cb][v];
@@ -250,10 +300,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       }
     }
   }
-  {
+  if (MODE == 1) {
     // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
     // hoisting all C * CB of them, which would spill the accumulators)
-    constexpr int NRES = C * CB, PF = 8;
+    constexpr int NRES = C * CB, PF = LNCH_PF;
     float4 rb[PF];
 #pragma unroll
     for (int i = 0; i < PF && i < NRES; ++i) rb[i] = ldh(i / CB, i % CB);
@@ -408,7 +458,7 @@ template <int N, int NWV>
 void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
                    float* h, int ne, int mode, hipStream_t s) {
   constexpr int C = 2 * N + 5;
-  const size_t smem = 2ull * 3 * C * LN_EPT * 64;
+  const size_t smem = 2ull * 3 * C * LN_EPT * 64 + ((LN_EPT + N - 1) / N + 1) * N * 16;
   const int grid = (ne + LN_EPT - 1) / LN_EPT;
   if (mode == 0) {
     ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);

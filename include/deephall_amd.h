@@ -349,6 +349,12 @@ int dh_debug_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const floa
                       const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3,
                       int ldp3, const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, void* stream);
 
+/* Fused channel GEMM + channel LayerNorm (gemm_lnch.hip; D = K = 256, N <= 6): in place over
+ * h [ne * (2N + 5)][256], mode 0: h = LN_ch(h + X W + b), mode 1: h = LN_ch(h + tanh_ch(h W + b))
+ * (X ignored); geo [ne][4] = (sin th, cos th, sin ph, cos ph) of the walkers' electrons. */
+int dh_debug_gemm_lnch(int N, int mode, const float* X, const uint16_t* Wp, int ldp, const float* bias,
+                       const float* ln, const float* geo, float* h, int ne, void* stream);
+
 /* Test hooks of the split-bf16 GEMM (gemm_x6.hip): the transposed weight Wt[ncols][K]
  * is split into three bf16 planes Wp[3][ldp][K] (ldp = dh_debug_x6_plane_rows(ncols),
  * uint16 bit patterns), then Y = X Wt^T (+ bias on rows r % C == 0) (+ R) with
