@@ -37,6 +37,9 @@
 #include "dh_internal.h"
 #include "device_common.h"
 
+#ifndef LNCH_SB
+#define LNCH_SB 1
+#endif
 #ifndef LNCH_PF
 #define LNCH_PF 8
 #endif
@@ -166,31 +169,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   auto sth = [&](int c, int cb, float4 v) {
     if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
   };
-  // MODE 0: the accumulators start from the residual h (+ the bias on the value rows), loaded
-  // here with the first activation loads, so the epilogue has no residual round trips
+  // the accumulators start from zero (the residual is added in the epilogue: starting them
+  // from h rounds every k-step's partial sum at |h| and measurably loosened the tangent
+  // channels against float64 on ill-conditioned walkers)
   f32x4 acc[C][CB];
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      if (MODE == 0) {
-        const float4 r = ldh(c, cb);
-        acc[c][cb] = (f32x4){r.x, r.y, r.z, r.w};
-      } else {
-        acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  if (MODE == 0 && bias) {
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      const float4 bv = *reinterpret_cast<const float4*>(bias + nf + 16 * cb);
-      acc[0][cb][0] += bv.x;
-      acc[0][cb][1] += bv.y;
-      acc[0][cb][2] += bv.z;
-      acc[0][cb][3] += bv.w;
-    }
-  }
-
+    for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
   {
     // column block outermost: one block's weight fragments (12 VGPRs) live at a time, the next
     // block's streaming in behind them; the activation fragments are re-read from LDS per block
@@ -239,7 +225,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
             split_store(ra, (kt + 1) & 1);
             if (kt + 2 < NK) load_a(kt + 2, ra);
           }
+#if LNCH_SB
           __builtin_amdgcn_sched_barrier(0);
+#endif
         }
 #pragma unroll
         for (int p = 0; p < 3; ++p) wf[p] = wn[p];
@@ -268,28 +256,32 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     if ((t & 1) == 0) return k == 0 ? -q.z : (k == 1 ? q.w : 0.f);
     return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
   };
-  // pre-LN rows x_c (in acc; MODE 0: complete): MODE 1's bias (value rows), tanh_ch, then + h
+  // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
+    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[0][cb][0] += bv.x;
+    acc[0][cb][1] += bv.y;
+    acc[0][cb][2] += bv.z;
+    acc[0][cb][3] += bv.w;
     if (MODE == 1) {
-      const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-      acc[0][cb][0] += bv.x;
-      acc[0][cb][1] += bv.y;
-      acc[0][cb][2] += bv.z;
-      acc[0][cb][3] += bv.w;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float z0 = acc[0][cb][v];
         const float y0 = tanhf(z0), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
         float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+        int gi = 0;
+        asm volatile("" : "+v"(gi));  // the geometry is re-read per feature, not held (spills)
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const float zt = acc[1 + t][cb][v];
-          sq = fmaf(zt, zt, sq);
-          u0 = fmaf(al(0, t), zt, u0);
-          u1 = fmaf(al(1, t), zt, u1);
-          u2 = fmaf(al(2, t), zt, u2);
-          acc[1 + t][cb][v] = d1 * zt;
+        for (int i = 0; i < N; ++i) {
+          const float4 q = gw[gi + i];
+          const float za = acc[1 + 2 * i][cb][v], zb = acc[2 + 2 * i][cb][v];
+          sq = fmaf(za, za, fmaf(zb, zb, sq));
+          u0 = fmaf(-q.z, za, fmaf(-(q.y * q.w), zb, u0));
+          u1 = fmaf(q.w, za, fmaf(-(q.y * q.z), zb, u1));
+          u2 = fmaf(q.x, zb, u2);
+          acc[1 + 2 * i][cb][v] = d1 * za;
+          acc[2 + 2 * i][cb][v] = d1 * zb;
         }
         acc[0][cb][v] = y0;
         acc[1 + T][cb][v] = d1 * acc[1 + T][cb][v] + d2 * sq;
@@ -300,7 +292,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       }
     }
   }
-  if (MODE == 1) {
+  {
     // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
     // hoisting all C * CB of them, which would spill the accumulators)
     constexpr int NRES = C * CB, PF = LNCH_PF;
