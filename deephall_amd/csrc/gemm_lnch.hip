@@ -37,6 +37,9 @@
 #include "dh_internal.h"
 #include "device_common.h"
 
+#ifndef LNCH_COUTER
+#define LNCH_COUTER 0
+#endif
 #ifndef LNCH_SB
 #define LNCH_SB 1
 #endif
@@ -178,6 +181,62 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
   {
+#if LNCH_COUTER
+    // channel outermost: each activation fragment read from LDS once per step and used by
+    // all CB column blocks (half the LDS reads of the block-outer order); all CB blocks'
+    // weight fragments live, the next step's streaming in behind them
+    float4 ra[NQ];
+    bf16x8 wf[CB][3], wn[CB][3];
+    load_a(0, ra);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) load_w(0, cb, wf[cb]);
+    split_store(ra, 0);
+    load_a(1, ra);
+#pragma unroll 1
+    for (int kt = 0; kt < NK; ++kt) {
+      __syncthreads();  // planes of step kt complete; step kt - 1's buffer is free
+      const char* P = smem + (kt & 1) * STAGE + xoff;
+      if (kt + 1 < NK) {
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) load_w(kt + 1, cb, wn[cb]);
+      }
+      bf16x8 xf[2][3];
+      auto ldx = [&](int c, bf16x8 (&x)[3]) {
+        x[0] = *reinterpret_cast<const bf16x8*>(P + c * EPT * 64);
+        x[1] = *reinterpret_cast<const bf16x8*>(P + PLANE + c * EPT * 64);
+        x[2] = *reinterpret_cast<const bf16x8*>(P + 2 * PLANE + c * EPT * 64);
+      };
+      ldx(0, xf[0]);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        if (c + 1 < C) ldx(c + 1, xf[(c + 1) & 1]);  // one channel ahead
+        const bf16x8 x0 = xf[c & 1][0], x1 = xf[c & 1][1], x2 = xf[c & 1][2];
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          f32x4 a = acc[c][cb];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x2, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][2], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][1], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][1], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x0, a, 0, 0, 0);
+          acc[c][cb] = a;
+        }
+        if (c == C / 2 && kt + 1 < NK) {
+          split_store(ra, (kt + 1) & 1);
+          if (kt + 2 < NK) load_a(kt + 2, ra);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (kt + 1 < NK) {
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) wf[cb][p] = wn[cb][p];
+      }
+    }
+  }
+#else
     // column block outermost: one block's weight fragments (12 VGPRs) live at a time, the next
     // block's streaming in behind them; the activation fragments are re-read from LDS per block
     float4 ra[NQ];
@@ -234,6 +293,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       }
     }
   }
+#endif
   __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
 #if LNCH_ABL & 1
   {  // ablation (tools only): no LayerNorm epilogue, the raw accumulators stored
