@@ -32,6 +32,11 @@
 // Traffic per launch: X once (the k loop), h once (the epilogue; in MODE 1 the same rows
 // as X, from MALL), h written once: 12 * rows * 256 B, against 20 (MODE 0) / 24 (MODE 1)
 // for the two-kernel form.
+//
+// Build knobs (tools/lnch_one.py A/B builds; defaults are the production kernel):
+// LNCH_COUTER channel-outer k loop; LNCH_SB per-channel sched barrier; LNCH_PF residual
+// loads in flight; LNCH_OPQ opaque residual offsets (register pressure); LNCH_ABL ablations
+// (bit 0: no LayerNorm epilogue, bit 1: no MFMAs — wrong results, timing only).
 #include <cstdlib>
 
 #include "dh_internal.h"
