@@ -87,3 +87,60 @@ def test_fused_matches_two_pass(cuda, tag, kw, B):
         print(f"{tag} {k} vs float64 (8 walkers): fused median {np.median(ef):.2e} max {ef.max():.2e} | "
               f"two-pass median {np.median(es):.2e} max {es.max():.2e}")
         assert np.median(ef) <= 3 * np.median(es) + 1e-6, (tag, k, ef, es)
+
+
+@pytest.mark.parametrize("N,B", [(3, 7), (6, 5), (6, 64)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kernel_vs_channel_oracle(cuda, N, B, mode):
+    """The kernel alone (dh_debug_gemm_lnch) against oracle/channels.py's float64 channel
+    rules: MODE 0 h <- LN_ch(h + X W + b), MODE 1 h <- LN_ch(h + tanh_ch(h W + b))
+    (psiformer.py:44-48), random rows / weights / geometry, partial last tiles (B N not a
+    multiple of 16).  Split-bf16 GEMM + f32 LN against the same op evaluated by torch in
+    float32: max error within 2x, median within 1.5x (measured: equal to within ~1.4x, e.g.
+    4.6e-5 vs 4.0e-5 max, 1.1e-7 vs 1.1e-7 median at N = 6)."""
+    import ctypes as C
+
+    from deephall_amd import _lib
+    from oracle import channels as CH
+
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(100 * N + B + mode)
+    Cc, D = 2 * N + 5, 256
+    X = torch.randn(B, N, Cc, D, generator=g, dtype=torch.float64)
+    h = torch.randn(B, N, Cc, D, generator=g, dtype=torch.float64)
+    W = torch.randn(D, D, generator=g, dtype=torch.float64) / 16
+    b = torch.randn(D, generator=g, dtype=torch.float64) * 0.1
+    scale = 1 + 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    bias = 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    x = torch.stack([torch.rand(B, N, generator=g, dtype=torch.float64) * 2.8 + 0.17,
+                     torch.rand(B, N, generator=g, dtype=torch.float64) * 6.28], -1)
+    X, h, W, b, scale, bias, x = (t.float().double() for t in (X, h, W, b, scale, bias, x))  # f32-representable
+    alpha = CH.geometry(x)["alpha"]
+
+    def ref(dt):
+        Xd, hd, Wd, bd, sd, bbd, ad = (t.to(dt) for t in (X, h, W, b, scale, bias, alpha))
+        if mode == 0:
+            pre = hd + CH.linear(Xd, Wd, bd)
+        else:
+            pre = hd + CH.tanh_ch(CH.linear(hd, Wd, bd), ad)
+        return CH.layer_norm_ch(pre, ad, sd, bbd)
+
+    y64, y32 = ref(torch.float64), ref(torch.float32).double()
+    dev = lambda t: t.float().contiguous().to(cuda)  # noqa: E731
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    hg, Xg = dev(h.reshape(-1, D)), dev(X.reshape(-1, D))
+    st, ct, sp, cp = (f(x[..., i]) for i, f in ((0, torch.sin), (0, torch.cos), (1, torch.sin), (1, torch.cos)))
+    geo = dev(torch.stack([st, ct, sp, cp], -1).reshape(-1, 4))
+    ldp = lib.dh_debug_x6_plane_rows(D)
+    Wp = torch.empty(3 * ldp * D, dtype=torch.int16, device=cuda)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.dh_debug_split_planes(p(dev(W.t())), D, D, D, p(Wp), s) == 0
+    ln = dev(torch.cat([scale, bias]))
+    assert lib.dh_debug_gemm_lnch(N, mode, p(Xg), p(Wp), ldp, p(dev(b)), p(ln), p(geo), p(hg), B * N, s) == 0
+    torch.cuda.synchronize()
+    got = hg.double().cpu().reshape(B, N, Cc, D)
+    err, err32 = (got - y64).abs(), (y32 - y64).abs()
+    print(f"N={N} B={B} mode={mode}: max err {err.max():.2e} (torch f32 {err32.max():.2e}), "
+          f"median {err.median():.2e} ({err32.median():.2e})")
+    assert err.max() <= 2 * err32.max() + 2e-6
+    assert err.median() <= 1.5 * err32.median() + 1e-8
