@@ -125,4 +125,35 @@ __device__ __forceinline__ float tanh_rat(float x) {
   return fabsf(x) < 4e-4f ? x : (c * p) * rq;
 }
 
+// tanhf with the device library's exact operation sequence (ROCm 7 ocml, gfx950 ISA of
+// tanhf: |x| < 0.625 odd polynomial in x^2, else 1 - 2 / (exp(2|x|) + 1) with exp from
+// v_exp_f32 + split log2(e) + ldexp), but both branches evaluated and selected: no
+// divergent control flow, so a register-heavy caller (gemm_lnch MODE 1) does not spill
+// around it.  Bit-identical to tanhf for every f32 (tools/tanh_exact.hip, exhaustive).
+__device__ __forceinline__ float tanh_ocml(float x) {
+#pragma clang fp contract(off)
+  const float y = fabsf(x);
+  // |x| >= 0.625
+  const float t = y + y;
+  const float p = t * 0x1.715476p+0f;  // log2(e) hi
+  const float r = __builtin_rintf(p);
+  const float f = p - r;
+  float e = __builtin_fmaf(t, 0x1.715476p+0f, -p);
+  e = __builtin_fmaf(t, 0x1.4ae0bep-26f, e);  // log2(e) lo
+  float v = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f + e), (int)r);
+  v = (t < -0x1.9d1da0p+6f) ? 0.f : v;
+  v = (t > 0x1.62e430p+6f) ? __builtin_inff() : v;
+  const float big = __builtin_fmaf(__builtin_amdgcn_rcpf(v + 1.f), -2.f, 1.f);
+  // |x| < 0.625
+  const float x2 = x * x;
+  float s = __builtin_fmaf(-0x1.758e7ap-8f, x2, 0x1.521192p-6f);
+  s = __builtin_fmaf(x2, s, -0x1.b8389cp-5f);
+  s = __builtin_fmaf(x2, s, 0x1.110704p-3f);
+  s = __builtin_fmaf(x2, s, -0x1.555532p-2f);
+  const float small = __builtin_fmaf(x2, y * s, y);
+  const float m = (y < 0.625f) ? small : big;
+  return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, m) & 0x7fffffffu) |
+                                       (__builtin_bit_cast(uint32_t, x) & 0x80000000u));
+}
+
 }  // namespace dh

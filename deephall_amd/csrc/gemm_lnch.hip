@@ -157,26 +157,6 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   };
   const int xoff = l16 * 64 + ((kg ^ lnch_sw(l16)) * 16);  // + c * EPT * 64 within a plane
 
-  // lane = electron l16 of the tile; its accumulators hold features nf + 16 cb + 0..3 of every
-  // channel row (MFMA D layout: col = lane & 15, row = 4 (lane >> 4) + reg)
-  const int E = e0 + l16;
-  const bool valid = E < ne;
-  const int b = (valid ? E : e0) / N;
-  const int nf = 16 * CB * wid + 4 * kg;  // + 16 cb
-  // this lane's rows of h (invalid electrons read the tile's first rows and store nothing);
-  // 32-bit offsets from the tile's base, each passed through an opaque asm so the compiler
-  // forms them one at a time (precomputing all 2 C row addresses spills)
-  char* const htile = reinterpret_cast<char*>(h + row0 * D);  // tile-uniform base (SGPRs)
-  const uint32_t hv = (uint32_t)(((valid ? l16 : 0) * C * D + nf) * 4);
-  auto roff = [&](int c, int cb) {  // 32-bit byte offset of (row c, block cb): saddr + voffset
-    uint32_t o = hv + (uint32_t)((c * D + 16 * cb) * 4);
-    asm volatile("" : "+v"(o));
-    return o;
-  };
-  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(htile + roff(c, cb)); };
-  auto sth = [&](int c, int cb, float4 v) {
-    if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
-  };
   // the accumulators start from zero (the residual is added in the epilogue: starting them
   // from h rounds every k-step's partial sum at |h| and measurably loosened the tangent
   // channels against float64 on ill-conditioned walkers)
@@ -300,6 +280,30 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   }
 #endif
   __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
+  // the epilogue's lane indices, re-derived from the lane id (mbcnt) rather than kept live
+  // across the k loop from threadIdx (holding them there made MODE 1 spill)
+  const int lane_e = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int l16e = lane_e & 15, kge = lane_e >> 4, tide = wid * 64 + lane_e;
+  // lane = electron l16 of the tile; its accumulators hold features nf + 16 cb + 0..3 of every
+  // channel row (MFMA D layout: col = lane & 15, row = 4 (lane >> 4) + reg)
+  const int E = e0 + l16e;
+  const bool valid = E < ne;
+  const int b = (valid ? E : e0) / N;
+  const int nf = 16 * CB * wid + 4 * kge;  // + 16 cb
+  // this lane's rows of h (invalid electrons read the tile's first rows and store nothing);
+  // 32-bit offsets from the tile's base, each passed through an opaque asm so the compiler
+  // forms them one at a time (precomputing all 2 C row addresses spills)
+  char* const htile = reinterpret_cast<char*>(h + row0 * D);  // tile-uniform base (SGPRs)
+  const uint32_t hv = (uint32_t)(((valid ? l16e : 0) * C * D + nf) * 4);
+  auto roff = [&](int c, int cb) {  // 32-bit byte offset of (row c, block cb): saddr + voffset
+    uint32_t o = hv + (uint32_t)((c * D + 16 * cb) * 4);
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(htile + roff(c, cb)); };
+  auto sth = [&](int c, int cb, float4 v) {
+    if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
+  };
 #if LNCH_ABL & 1
   {  // ablation (tools only): no LayerNorm epilogue, the raw accumulators stored
     const int E = e0 + l16;
@@ -330,10 +334,16 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     acc[0][cb][2] += bv.z;
     acc[0][cb][3] += bv.w;
     if (MODE == 1) {
+      // the value row's tanh first, one feature at a time (its temporaries never overlap
+      // the channel algebra's); tanh_ocml = tanhf bit for bit, without tanhf's branch
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const float z0 = acc[0][cb][v];
-        const float y0 = tanhf(z0), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
+        acc[0][cb][v] = tanh_ocml(acc[0][cb][v]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float y0 = acc[0][cb][v], d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
         float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
         int gi = 0;
         asm volatile("" : "+v"(gi));  // the geometry is re-read per feature, not held (spills)
@@ -348,7 +358,6 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           acc[1 + 2 * i][cb][v] = d1 * za;
           acc[2 + 2 * i][cb][v] = d1 * zb;
         }
-        acc[0][cb][v] = y0;
         acc[1 + T][cb][v] = d1 * acc[1 + T][cb][v] + d2 * sq;
         acc[2 + T][cb][v] = d1 * acc[2 + T][cb][v] + d2 * (u0 * u0);
         acc[3 + T][cb][v] = d1 * acc[3 + T][cb][v] + d2 * (u1 * u1);
@@ -391,11 +400,11 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     constexpr int NS = decltype(NS_)::value;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      red[(wid * NS + j) * 64 + lane] = part(j);  // every lane's 8-feature partial (no cross-lane ops)
+      red[(wid * NS + j) * 64 + lane_e] = part(j);  // every lane's 8-feature partial (no cross-lane ops)
       __builtin_amdgcn_sched_barrier(0);          // one statistic at a time (register pressure)
     }
     __syncthreads();
-    for (int i = tid; i < NS * EPT; i += NT) {
+    for (int i = tide; i < NS * EPT; i += NT) {
       const int j = i / EPT, e = i - j * EPT;
       float s = 0.f;
 #pragma unroll
@@ -406,7 +415,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     }
     __syncthreads();
   };
-  const float* mt = tot + l16 * TS;  // this lane's electron
+  const float* mt = tot + l16e * TS;  // this lane's electron
   // channel means, centre
   reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
 #pragma unroll
