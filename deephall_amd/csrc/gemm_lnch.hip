@@ -36,7 +36,8 @@
 // Build knobs (tools/lnch_one.py A/B builds; defaults are the production kernel):
 // LNCH_COUTER channel-outer k loop; LNCH_SB per-channel sched barrier; LNCH_PF residual
 // loads in flight; LNCH_OPQ opaque residual offsets (register pressure); LNCH_ABL ablations
-// (bit 0: no LayerNorm epilogue, bit 1: no MFMAs — wrong results, timing only).
+// (bit 0: no LayerNorm epilogue, bit 1: no MFMAs — wrong results, timing only); LNCH_RPF MODE 0
+// residual-line touch during the k loop.
 #include <cstdlib>
 
 #include "dh_internal.h"
@@ -56,6 +57,9 @@
 #endif
 #ifndef LNCH_OPQ
 #define LNCH_OPQ 1
+#endif
+#ifndef LNCH_RPF
+#define LNCH_RPF 0
 #endif
 
 namespace dh {
@@ -226,6 +230,13 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     // block's streaming in behind them; the activation fragments are re-read from LDS per block
     float4 ra[NQ];
     bf16x8 wf[3], wn[3];
+    // MODE 0 (X = o, not h): one dword of every 128-B line of the tile's residual rows is
+    // touched during the k loop (one line per thread per step), so the epilogue's residual
+    // loads find the lines in the MALL / L2 instead of HBM; the touched values are folded
+    // into an opaque word, consumed a step later (the load never stalls the loop)
+    constexpr int RLINES = ROWS * D * 4 / 128;
+    const auto rsH = __builtin_amdgcn_make_buffer_rsrc(h + row0 * D, (short)0, tbytes, 0x00020000);
+    uint32_t rpf = 0, rpv = 0;
     load_a(0, ra);
     load_w(0, 0, wf);
     split_store(ra, 0);
@@ -268,6 +279,11 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           if (cb == 0 && c == C / 2 && kt + 1 < NK) {
             split_store(ra, (kt + 1) & 1);
             if (kt + 2 < NK) load_a(kt + 2, ra);
+            if (MODE == 0 && LNCH_RPF) {
+              rpf ^= rpv;
+              const int li = kt * NT + tid;
+              rpv = li < RLINES ? __builtin_amdgcn_raw_buffer_load_b32(rsH, li * 128, 0, 0) : 0u;
+            }
           }
 #if LNCH_SB
           __builtin_amdgcn_sched_barrier(0);
@@ -277,6 +293,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         for (int p = 0; p < 3; ++p) wf[p] = wn[p];
       }
     }
+    if (MODE == 0 && LNCH_RPF && (rpf ^ rpv) == 0x7fc00001u && ne < 0) h[0] = 0.f;  // never taken
   }
 #endif
   __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
