@@ -2,7 +2,9 @@
 
 from __future__ import annotations
 
+import json
 import math
+import os
 
 import numpy as np
 import torch
@@ -97,18 +99,30 @@ def logpsi_f32_errors(p64, cfg, x):
 
 FLOOR_X = 1.5        # median: at most 1.5x the float32 run's
 FLOOR_X_P90 = 2.0    # 90th percentile (the 3rd-4th worst of 32 walkers: conditioning-dominated)
-FLOOR_X_MAX = 6.0    # the single worst walker (an ill-conditioned orbital matrix dominates it)
+FLOOR_X_MAX = 4.0    # the single worst walker (an ill-conditioned orbital matrix dominates it);
+# measured on the MI355X (tools/r03_floor_survey.sh, profiles/r03_floor_survey.txt): at most
+# 2.97x over every gate the ratio decides, except the near-pole fixtures
+FLOOR_X_MAX_POLE = 6.0  # theta within 0.15 rad of a pole: 1/sin(theta) amplifies both runs (5.2x measured)
 FLOOR_SLACK = 2e-7   # observables the float32 run happens to get (nearly) exact
 
 
-def within_f32_floor(err_hip, err_f32, floor_abs=0.0):
+def within_f32_floor(err_hip, err_f32, floor_abs=0.0, max_x=None):
     """The kernels' per-walker errors are at or below the float32 run's error distribution:
     median within FLOOR_X, 90th percentile within FLOOR_X_P90 of the float32 run's, the
-    maximum within FLOOR_X_MAX, or everything below ``floor_abs`` (e.g. north_star's 1e-5)."""
+    maximum within FLOOR_X_MAX (``max_x`` where given), or everything below ``floor_abs``
+    (e.g. north_star's 1e-5)."""
     e, f = np.asarray(err_hip, np.float64), np.asarray(err_f32, np.float64)
+    log = os.environ.get("DH_FLOOR_LOG")
+    if log:  # margin survey (tools): the three ratios of every gate evaluation
+        with open(log, "a") as fh:
+            fh.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "?"),
+                                 "med": float(np.median(e) / max(np.median(f), 1e-30)),
+                                 "p90": float(np.percentile(e, 90) / max(np.percentile(f, 90), 1e-30)),
+                                 "max": float(e.max() / max(f.max(), 1e-30)),
+                                 "emax": float(e.max()), "fmax": float(f.max()), "floor_abs": floor_abs}) + "\n")
     if e.max() <= floor_abs:
         return True
     ok = np.median(e) <= FLOOR_X * np.median(f) + FLOOR_SLACK
     ok &= np.percentile(e, 90) <= FLOOR_X_P90 * np.percentile(f, 90) + FLOOR_SLACK
-    ok &= e.max() <= FLOOR_X_MAX * f.max() + FLOOR_SLACK
+    ok &= e.max() <= (FLOOR_X_MAX if max_x is None else max_x) * f.max() + FLOOR_SLACK
     return bool(ok)

@@ -6,8 +6,8 @@ fixture (tests/golden/make_golden.py, round2) holds the float64 restatement's va
 the same full-Hessian algorithm run in float32 on the same walkers and parameters.  Per
 observable the HIP errors (relative, floor 1) must sit at or below that float32 run's
 error distribution (helpers.within_f32_floor): median within 1.5x, 90th percentile
-within 2x, the single worst walker within 6x (an ill-conditioned orbital matrix dominates it, and
-two independent f32 rounding draws differ there), 2e-7 slack; log psi and its phase pass
+within 2x, the single worst walker within 4x (6x for the near-pole fixtures: an ill-conditioned
+orbital matrix dominates it, and two independent f32 rounding draws differ there), 2e-7 slack; log psi and its phase pass
 outright when every walker is within 1e-5.  The fixtures cover near-pole walkers
 (theta in [1e-3, 0.15] and pi minus that), the harmonic potential, an explicit radius,
 and 32-walker batches at C2, C4 and C5.  Every test prints the per-observable max and
@@ -24,7 +24,7 @@ import pytest
 import torch
 
 from deephall_amd import hamiltonian
-from helpers import make_params, to_device_params, within_f32_floor
+from helpers import FLOOR_X_MAX, FLOOR_X_MAX_POLE, make_params, to_device_params, within_f32_floor
 from oracle import reference as R
 from test_gpu_parity import build
 
@@ -57,15 +57,16 @@ def test_within_float32_floor(cuda, tag):
     e, o = hamiltonian.local_energy(model, system)(params, x)
     got = {"e_l": e.cpu().numpy(), **{k: o[v].cpu().numpy() for k, v in OBS[1:]}, "potential": o["potential"].cpu().numpy()}
     rows, fails = [], []
+    max_x = FLOOR_X_MAX_POLE if tag.endswith("_pole") else FLOOR_X_MAX
     # log psi: 1e-5 relative, or the float32 run's own error where that is larger
     err_lp = rel(lp.real, g["logpsi"].real)
     err_lp32 = rel(g["logpsi32"].real, g["logpsi"].real)
     rows.append(("logpsi", err_lp, err_lp32))
-    if not within_f32_floor(err_lp, err_lp32, 1e-5):
+    if not within_f32_floor(err_lp, err_lp32, 1e-5, max_x):
         fails.append("logpsi")
     dphi = np.abs(np.angle(np.exp(1j * (lp.imag - g["logpsi"].imag))))
     dphi32 = np.abs(np.angle(np.exp(1j * (g["logpsi32"].imag - g["logpsi"].imag))))
-    if not within_f32_floor(dphi, dphi32, 1e-5):
+    if not within_f32_floor(dphi, dphi32, 1e-5, max_x):
         fails.append("phase")
     if not rel(got["potential"], g["potential"]).max() < 1e-5:
         fails.append("potential")
@@ -73,7 +74,7 @@ def test_within_float32_floor(cuda, tag):
         ref, r32 = g[key], g[key + "32"]
         eh, e32 = rel(got[key], ref), rel(r32, ref)
         rows.append((key, eh, e32))
-        if not within_f32_floor(eh, e32):
+        if not within_f32_floor(eh, e32, 0.0, max_x):
             fails.append(key)
     rows.insert(1, ("phase", dphi, dphi32))
     print(f"\n{tag}: observable | HIP max p90 median | float32 run max p90 median  (relative, floor 1)")
