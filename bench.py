@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="do not record per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--mcmc-calls", type=int, default=20, help="timed mcmc_step calls for walker_steps_per_sec")
+    ap.add_argument("--extra-configs", default="C4,C5",
+                    help="comma list of EXTRA_CONFIGS also timed (one-GPU lines in configs_1gpu; '' = none)")
+    ap.add_argument("--extra-steps", type=int, default=3)
+    ap.add_argument("--extra-warmup", type=int, default=2)
     ap.add_argument("--cpu-c1-seconds", type=float, default=6.0,
                     help="CPU-baseline budget for BASELINE.json configs[0] (N=3 2Q=2, B=100)")
     return ap.parse_args()
@@ -85,24 +89,12 @@ def spawn_ranks(n: int) -> int:
     return max(abs(rc) for rc in rcs)
 
 
-def main():
-    args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
-    # DH_BENCH_BACKEND=gloo, DH_BENCH_ONE_GPU=1 puts every rank on device 0
-    if os.environ.get("DH_BENCH_ONE_GPU"):
-        local = 0
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("DH_BENCH_BACKEND", "nccl"))
-    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+EXTRA_CONFIGS = {"C4": ((10, 0), 23), "C5": ((20, 0), 57)}  # BASELINE.json configs[3], [4]
 
+
+def run_workload(args, dev, rank, world, nspins, flux, B, n_steps, n_warmup, burn_in, instrument, components):
+    """One workload: burn-in, W warmup VMC steps, exactly K timed steps (barrier + sync on both
+    sides, max over ranks), then the instrumented region and the component timings."""
     from deephall_amd import _lib, config
     from deephall_amd.hamiltonian import _run_local_energy
     from deephall_amd.loss import device_stats, reduce_stats
@@ -113,10 +105,9 @@ def main():
     from deephall_amd.train import init_guess, make_vmc_iteration
 
     lib = _lib.load()
-    system = config.System(nspins=tuple(args.nspins), flux=args.flux)
+    system = config.System(nspins=tuple(nspins), flux=flux)
     model = make_network(system, config.Network())
-    B = args.batch
-    N = sum(args.nspins)
+    N = sum(nspins)
     params = model.init(PRNGKey(42), device=dev)
     data = init_guess(Key(4242), B, N, dev, walker_offset=rank * B, network=model)
     steps = args.mcmc_steps
@@ -143,10 +134,10 @@ def main():
         t_iter[0] += 1
         return data, stats
 
-    for _ in range(args.burn_in):
+    for _ in range(burn_in):
         data, _ = mcmc_step(params, data, key, width, reduce=False)
         key = key.advance(steps)
-    for _ in range(args.warmup):
+    for _ in range(n_warmup):
         data, stats = vmc_step(data, key)
         key = key.advance(steps)
     h = get_handle(model.spec, dev)
@@ -159,7 +150,7 @@ def main():
     # ---------------- timed region: exactly K steps, no instrumentation
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(n_steps):
         data, stats = vmc_step(data, key)
         key = key.advance(steps)
     barrier()
@@ -180,11 +171,11 @@ def main():
 
     prof = (C.c_double * (4 * len(_lib.PROF_KINDS)))()
     dt_prof = float("nan")
-    if not args.no_kernel_events:
+    if instrument:
         lib.dh_profile_enable(h.h, 1)
         barrier()
         a = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(n_steps):
             data, _ = vmc_step(data, key, iteration1)  # kernels one at a time: clean durations
             key = key.advance(steps)
         barrier()
@@ -195,7 +186,7 @@ def main():
     # ---------------- MCMC walker-steps/s: >= 20 mcmc_step calls, each with
     # its pmove all-reduce and the host read of pmove; then the E_L-only rate
     t_mcmc = t_el = float("nan")
-    if not args.no_components:
+    if components:
         barrier()
         a = time.perf_counter()
         for _ in range(args.mcmc_calls):
@@ -214,38 +205,30 @@ def main():
         barrier()
         t_el = (time.perf_counter() - a) / 3
 
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-    kinds = _lib.PROF_KINDS
+    return dict(dt=dt, dt_prof=dt_prof, prof=list(prof), t_mcmc=t_mcmc, t_el=t_el, energy=energy, pmove=pmove)
+
+
+def kernels_of(prof, n_steps):
+    from deephall_amd import _lib
+
     kern = {}
-    for i, k in enumerate(kinds):
+    for i, k in enumerate(_lib.PROF_KINDS):
         cnt, ms, fl, by = prof[4 * i : 4 * i + 4]
         if cnt:
-            kern[k] = {
-                "launches_per_step": cnt / args.steps,
-                "ms_per_step": ms / args.steps,
-                "avg_us": 1e3 * ms / cnt,
-            }
-    from deephall_amd.networks import psiformer as _pf
+            kern[k] = {"launches_per_step": cnt / n_steps, "ms_per_step": ms / n_steps, "avg_us": 1e3 * ms / cnt}
+    return kern
 
-    gemm_mode = _pf._GEMM_MODE
-    x6 = gemm_mode in ("x6", "x6all")
-    # HBM traffic per channel-GEMM launch: rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate
-    # passes) of this same workload, committed by tools/profile_round.sh; default config only
-    traffic = traffic_src = None
-    tf = ROOT / "profiles" / "gemm_traffic.json"
-    if tf.exists() and (B, tuple(args.nspins), args.flux, steps) == (4096, (6, 0), 15, 10):
-        tj = json.loads(tf.read_text())
-        traffic = tj.get("channel_gemm_bytes_per_launch") if x6 else None
-        traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})" if traffic else None
-    # dominant kernel: the local-energy channel GEMM (class gemm_ch of dh_profile_read; in
-    # the split-bf16 modes gemm_x6m_kernel for the wide maps and gemm_lnch_kernel, GEMM +
-    # channel LayerNorm, for the 256-column ones).  Its arithmetic
-    # runs as 6 bf16 MFMA products per f32 product, so the ceiling of its algorithmic f32
-    # flop rate is the dense bf16 MFMA peak / 6.  The log-psi GEMMs (class gemm: exact-f32
-    # gemm_ln_kernel + split-bf16 gemm_x6d_kernel) are reported beside it.
+
+def roofline_of(prof, n_steps, dt_prof, x6, traffic=None, traffic_src=None):
+    """Dominant kernel class: the local-energy channel GEMMs (class gemm_ch of dh_profile_read; in
+    the split-bf16 modes gemm_x6m_kernel for the wide maps and gemm_lnch_kernel, GEMM + channel
+    LayerNorm, for the 256-column ones at N <= 6).  Its arithmetic runs as 6 bf16 MFMA products per
+    f32 product, so the ceiling of its algorithmic f32 flop rate is the dense bf16 MFMA peak / 6.
+    The log-psi GEMMs (class gemm) are reported beside it."""
+    from deephall_amd import _lib
+
+    kinds = _lib.PROF_KINDS
+
     def _cls(name):
         i = kinds.index(name)
         return prof[4 * i], prof[4 * i + 1], prof[4 * i + 2], prof[4 * i + 3]
@@ -254,7 +237,7 @@ def main():
     l_cnt, l_ms, l_fl, l_by = _cls("gemm")
     achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
     peak = PEAK_BF16_MFMA_TFLOPS / 6 if x6 else PEAK_F32_MFMA_TFLOPS
-    roofline = {
+    return {
         "kernel": ("local-energy channel GEMMs, split-bf16 f32 GEMM (v_mfma_f32_16x16x32_bf16): "
                    "gemm_x6m_kernel (q|k|v and orbital maps) + gemm_lnch_kernel (the 256-column maps "
                    "with the channel LayerNorm fused in; its LN work counted in the launch time, not "
@@ -272,19 +255,79 @@ def main():
         "flops_per_launch": g_fl / g_cnt if g_cnt else 0,
         "avg_launch_us": 1e3 * g_ms / g_cnt if g_cnt else 0,
         "share_of_step": round(g_ms / (dt_prof * 1e3), 4) if g_ms else None,
-        "measured_over": f"{args.steps} instrumented VMC steps (HIP event pair per launch)",
+        "measured_over": f"{n_steps} instrumented VMC steps (HIP event pair per launch)",
         "traffic_source": traffic_src,
         "bytes_per_launch_algorithmic": g_by / g_cnt if g_cnt else 0,
         "logpsi_gemms": {
-            "launches_per_step": l_cnt / args.steps,
+            "launches_per_step": l_cnt / n_steps,
             "avg_launch_us": 1e3 * l_ms / l_cnt if l_cnt else 0,
             "achieved_tflops": round((l_fl / (l_ms * 1e-3)) / 1e12, 2) if l_ms > 0 else 0.0,
             "share_of_step": round(l_ms / (dt_prof * 1e3), 4) if l_ms else None,
         },
-    } if not args.no_kernel_events else None
+    }
+
+
+def f_fwd(N, flux):
+    """Forward flops per walker, default Psiformer (D = 256, 2 layers, 1 det)."""
+    return 2 * N * 4 * 256 + 2 * (12 * N * 256**2 + 4 * N * N * 256) + 4 * N * 256 * (flux + 1) * N
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
+    # DH_BENCH_BACKEND=gloo, DH_BENCH_ONE_GPU=1 puts every rank on device 0
+    if os.environ.get("DH_BENCH_ONE_GPU"):
+        local = 0
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(os.environ.get("DH_BENCH_BACKEND", "nccl"))
+    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+
+
+    B = args.batch
+    N = sum(args.nspins)
+    r = run_workload(args, dev, rank, world, tuple(args.nspins), args.flux, B, args.steps, args.warmup,
+                     args.burn_in, not args.no_kernel_events, not args.no_components)
+    dt, dt_prof, prof, t_mcmc, t_el = r["dt"], r["dt_prof"], r["prof"], r["t_mcmc"], r["t_el"]
+    energy, pmove = r["energy"], r["pmove"]
+    steps = args.mcmc_steps
+    # the other BASELINE.json configs with a larger N (configs[3] N=10 2Q=23, configs[4] N=20 2Q=57),
+    # one-GPU weak-scaling lines of the same VMC iteration (4096 walkers per GPU), a few steps each
+    extra = {}
+    if args.extra_configs:
+        for tag in args.extra_configs.split(","):
+            nsp, fx = EXTRA_CONFIGS[tag]
+            rx = run_workload(args, dev, rank, world, nsp, fx, B, args.extra_steps, args.extra_warmup, 2,
+                              not args.no_kernel_events, False)
+            extra[tag] = (nsp, fx, rx)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    kern = kernels_of(prof, args.steps)
+    from deephall_amd.networks import psiformer as _pf
+
+    gemm_mode = _pf._GEMM_MODE
+    x6 = gemm_mode in ("x6", "x6all")
+    # HBM traffic per channel-GEMM launch: rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate
+    # passes) of this same workload, committed by tools/profile_round.sh; default config only
+    traffic = traffic_src = None
+    tf = ROOT / "profiles" / "gemm_traffic.json"
+    if tf.exists() and (B, tuple(args.nspins), args.flux, steps) == (4096, (6, 0), 15, 10):
+        tj = json.loads(tf.read_text())
+        traffic = tj.get("channel_gemm_bytes_per_launch") if x6 else None
+        traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})" if traffic else None
+    roofline = roofline_of(prof, args.steps, dt_prof, x6, traffic, traffic_src) if not args.no_kernel_events else None
     B_total = B * world
     value = B_total * args.steps / dt
-    F_fwd = 2 * N * 4 * 256 + 2 * (12 * N * 256**2 + 4 * N * N * 256) + 4 * N * 256 * (args.flux + 1) * N
+    F_fwd = f_fwd(N, args.flux)
     metric = METRIC.format(N=N, flux=args.flux)
     out = {
         "metric": metric,
@@ -324,6 +367,27 @@ def main():
         "energy": [round(energy.real, 5), round(energy.imag, 5)],
         "pmove": round(pmove, 3),
     }
+    if extra:
+        out["configs_1gpu"] = {}
+        for tag, (nsp, fx, rx) in extra.items():
+            n = sum(nsp)
+            rl = roofline_of(rx["prof"], args.extra_steps, rx["dt_prof"], x6) if not args.no_kernel_events else None
+            out["configs_1gpu"][tag] = {
+                "config": f"nspins={list(nsp)} flux={fx} (BASELINE.json configs[{3 if tag == 'C4' else 4}], "
+                          f"{B} walkers per GPU, weak scaling)",
+                "value": round(B_total * args.extra_steps / rx["dt"], 1),
+                "unit": "local-energies/s",
+                "steps": args.extra_steps,
+                "warmup": args.extra_warmup,
+                "ms_per_step": round(1e3 * rx["dt"] / args.extra_steps, 3),
+                "roofline": {k: rl[k] for k in ("bound", "achieved", "peak", "unit", "frac", "avg_launch_us",
+                                                "flops_per_launch", "share_of_step")} if rl else None,
+                "kernels_ms_per_step": {k: round(v["ms_per_step"], 3)
+                                        for k, v in kernels_of(rx["prof"], args.extra_steps).items()},
+                "energy": [round(rx["energy"].real, 5), round(rx["energy"].imag, 5)],
+                "model_tflops_step": round(B_total * (2 * n + 5 + args.mcmc_steps + 1) * f_fwd(n, fx)
+                                           / rx["dt"] * args.extra_steps / 1e12, 2),
+            }
     if world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
         from oracle.reference import OracleConfig

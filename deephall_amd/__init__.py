@@ -7,7 +7,7 @@ Public names mirror the reference package:
   make_local_kinetic_energy, make_potential
   make_mcmc_step, update_mcmc_width   deephall.mcmc
   make_loss_fn, LossMode              deephall.loss (statistics + parameter gradient)
-  make_optimizer_step                 deephall.optimizers (Adam, none)
+  make_optimizer_step                 deephall.optimizers (KFAC = the default, Adam, none)
   train, init_guess, initalize_state, setup_mcmc, vmc   deephall.train
 All compute runs in the HIP library deephall_amd/_lib/libdeephall_amd.so.
 """

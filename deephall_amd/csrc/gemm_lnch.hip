@@ -61,8 +61,37 @@
 #ifndef LNCH_RPF
 #define LNCH_RPF 0
 #endif
+#ifndef LNCH_RDMA
+#define LNCH_RDMA 1
+#endif
+#ifndef LNCH_RDMA_LATE
+#define LNCH_RDMA_LATE 1
+#endif
+#ifndef LNCH_STAMP
+#define LNCH_STAMP 0
+#endif
 
 namespace dh {
+
+#if LNCH_STAMP
+// diagnostic builds only (tools/lnch_one.py): per-workgroup phase timestamps (s_memtime) of
+// the first LNCH_STAMP_WG tiles, written by thread 0 into a buffer nothing else reads
+constexpr int LNCH_STAMP_WG = 4096, LNCH_NSTAMP = 10;
+__device__ unsigned long long g_lnch_stamp[LNCH_STAMP_WG * LNCH_NSTAMP];
+#define LNCH_T(i)                                                                    \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG)                              \
+      g_lnch_stamp[blockIdx.x * LNCH_NSTAMP + (i)] = __builtin_amdgcn_s_memtime();   \
+  } while (0)
+#define LNCH_RT(i)                                                                   \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG)                              \
+      g_lnch_stamp[blockIdx.x * LNCH_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LNCH_T(i)
+#define LNCH_RT(i)
+#endif
 
 namespace {
 
@@ -75,6 +104,18 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
 constexpr int LN_D = 256;   // features (= K)
 constexpr int LN_BK = 32;   // k per step
+// epilogue residual through LDS (LNCH_RDMA): chunks of LN_RCH channel rows of all 16
+// electrons (LN_RCH * 16 rows of 1 KB), two chunk buffers
+constexpr int LN_RCH = 4;
+constexpr int LN_RBUF = LN_RCH * LN_EPT * LN_D * 4;  // bytes of one chunk buffer
+
+// LDS bytes of the kernel: the two k-step plane stages (reused by the epilogue's residual
+// chunks and statistics), then the walkers' geometry
+__host__ __device__ constexpr int lnch_geo_off(int N) {
+  return (6 * (2 * N + 5) * LN_EPT * 64 > (LNCH_RDMA ? 2 * LN_RBUF : 0)) ? 6 * (2 * N + 5) * LN_EPT * 64
+                                                                       : 2 * LN_RBUF;
+}
+__host__ __device__ constexpr int lnch_smem(int N) { return lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16; }
 
 __device__ __forceinline__ uint32_t pkbf(float x, float y) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
@@ -96,7 +137,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   constexpr int NQ = (ROWS * 8 + NT - 1) / NT;     // 16-B activation pieces per thread per step
   constexpr int NR = C + T + 3;                    // second-moment statistics per electron
   constexpr int TS = NR | 1;                       // odd row stride of the totals
-  static_assert(2 * STAGE + ((EPT + N - 1) / N + 1) * N * 16 <= 163840, "LDS");
+  static_assert(2 * STAGE <= lnch_geo_off(N) && lnch_smem(N) <= 163840, "LDS");
   static_assert(NWV * NR * 64 * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
@@ -107,11 +148,13 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const int e0 = tile * EPT;                       // first electron of the tile
   const size_t row0 = (size_t)e0 * C;
   const int rows_valid = min(ROWS, (ne - e0) * C);
+  LNCH_T(0);
+  LNCH_RT(8);
 
   // geometry of the walkers the tile's electrons belong to, staged once in LDS past the
   // stage buffers (visible after the k loop's barriers)
   constexpr int GW = (EPT + N - 1) / N + 1;  // walkers a 16-electron tile can touch
-  float4* gl = reinterpret_cast<float4*>(smem + 2 * STAGE);
+  float4* gl = reinterpret_cast<float4*>(smem + lnch_geo_off(N));
   if (tid < GW * N) {
     const int ge = (e0 / N) * N + tid;
     gl[tid] = ge < ne ? reinterpret_cast<const float4*>(geo)[ge] : make_float4(0.f, 1.f, 0.f, 1.f);
@@ -244,6 +287,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll 1
     for (int kt = 0; kt < NK; ++kt) {
       __syncthreads();  // planes of step kt complete; step kt - 1's buffer is free
+      if (kt == 0) LNCH_T(1);
       const char* P = smem + (kt & 1) * STAGE + xoff;
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
@@ -297,9 +341,50 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   }
 #endif
   __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
+  LNCH_T(2);
   // the epilogue's lane indices, re-derived from the lane id (mbcnt) rather than kept live
   // across the k loop from threadIdx (holding them there made MODE 1 spill)
   const int lane_e = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#if LNCH_RDMA
+  // ---- the residual rows h through LDS by DMA (global_load_lds_dwordx4, no VGPRs): chunk k =
+  // channel rows LN_RCH k .. + LN_RCH - 1 of the tile's 16 electrons, one 1-KB row per wave
+  // instruction, into chunk buffer k & 1 at row q = (c - LN_RCH k) * 16 + e.  16-B slot s of
+  // a row holds the row's quad s ^ e (the swizzle is on the SOURCE address: the DMA writes
+  // lane-linearly), so the epilogue's ds_read_b128 of quad Q = 8 w + 4 cb + g by lane (e, g)
+  // hits slot Q ^ e: 16 distinct slots in every lane group.  Rows of electrons past the end
+  // re-read the tile's first row into their (never read) slot, so every wave issues the same
+  // compile-time number of DMAs per chunk and "chunk k landed" is vmcnt(DMAs of chunk k + 1).
+  constexpr int NCHK = (C + LN_RCH - 1) / LN_RCH;
+  auto rows_of = [](int k) { return EPT * (C - LN_RCH * k < LN_RCH ? C - LN_RCH * k : LN_RCH); };
+  static_assert(EPT * LN_RCH % NWV == 0 && EPT % NWV == 0, "DMA rows must divide over the waves");
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto rdma = [&](int k) {
+    const int nrow = rows_of(k);
+#pragma unroll
+    for (int j = 0; j < LN_RCH * EPT / NWV; ++j) {
+      const int q = wid + NWV * j;  // wave-uniform
+      if (q < nrow) {
+        const int c = LN_RCH * k + q / EPT, e = q % EPT;
+        const int er = e0 + e < ne ? e : 0;
+        // row base in SGPRs, the lane's swizzled 16-B quad as a 32-bit VGPR offset (formed here,
+        // not hoisted: 64-bit per-lane addresses of every chunk held across the epilogue spill)
+        const float* rowp = h + (row0 + (size_t)(er * C + c)) * D;
+        uint32_t voff = (uint32_t)(lane_e ^ e) << 4;
+        asm volatile("" : "+v"(voff));
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((k & 1) * LN_RBUF + q * D * 4));
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rowp), "s"(dst)
+                     : "memory");
+      }
+    }
+  };
+  if (MODE == 0 || !LNCH_RDMA_LATE) {
+    rdma(0);
+    if (NCHK > 1) rdma(1);
+  }
+#endif
   const int l16e = lane_e & 15, kge = lane_e >> 4, tide = wid * 64 + lane_e;
   // lane = electron l16 of the tile; its accumulators hold features nf + 16 cb + 0..3 of every
   // channel row (MFMA D layout: col = lane & 15, row = 4 (lane >> 4) + reg)
@@ -317,7 +402,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     asm volatile("" : "+v"(o));
     return o;
   };
+#if !LNCH_RDMA
   auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(htile + roff(c, cb)); };
+#endif
   auto sth = [&](int c, int cb, float4 v) {
     if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
   };
@@ -343,6 +430,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
   };
   // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
+  float chain = 0.f;
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
     const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -362,8 +450,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       for (int v = 0; v < 4; ++v) {
         const float y0 = acc[0][cb][v], d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
         float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+        // the geometry is re-read per feature, not held (spills): its offset is opaque and
+        // depends on the previous feature's last result, so the reads cannot be batched early
         int gi = 0;
-        asm volatile("" : "+v"(gi));  // the geometry is re-read per feature, not held (spills)
+        asm volatile("" : "+v"(gi) : "v"(y0), "v"(chain));
 #pragma unroll
         for (int i = 0; i < N; ++i) {
           const float4 q = gw[gi + i];
@@ -379,10 +469,65 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         acc[2 + T][cb][v] = d1 * acc[2 + T][cb][v] + d2 * (u0 * u0);
         acc[3 + T][cb][v] = d1 * acc[3 + T][cb][v] + d2 * (u1 * u1);
         acc[4 + T][cb][v] = d1 * acc[4 + T][cb][v] + d2 * (u2 * u2);
+        chain = acc[4 + T][cb][v];
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
+#if LNCH_RDMA
+  if (MODE == 1) {
+    // the tanh_ch results are materialised here, before the DMA blocks (otherwise the
+    // compiler sinks the channel algebra past them and its live ranges spill)
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) asm volatile("" : "+v"(acc[c][cb]));
+  }
+  if (MODE == 1 && LNCH_RDMA_LATE) {
+    rdma(0);
+    if (NCHK > 1) rdma(1);
+  }
+  {
+    // this lane's row in a chunk buffer (+ channel / buffer offsets) and its two quad slots
+    const char* const rb0 = smem + l16e * D * 4;
+    int rsl[CB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) rsl[cb] = 16 * ((4 * CB * wid + 4 * cb + kge) ^ l16e);
+#pragma unroll
+    for (int k = 0; k < NCHK; ++k) {
+      // this wave's chunk-k DMAs landed (the younger ones are chunk k + 1's), then every wave's
+      if (k + 1 < NCHK)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(rows_of(k + 1) / NWV) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int cc = 0; cc < LN_RCH; ++cc) {
+        const int c = LN_RCH * k + cc;
+        if (c < C) {
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            const float4 r = *reinterpret_cast<const float4*>(rb0 + (k & 1) * LN_RBUF + cc * EPT * D * 4 + rsl[cb]);
+            f32x4& a = acc[c][cb];
+            a[0] = r.x + a[0];
+            a[1] = r.y + a[1];
+            a[2] = r.z + a[2];
+            a[3] = r.w + a[3];
+#if LNCH_OPQ
+            asm volatile("" : "+v"(a));  // consumed here (keeps the reads from being batched)
+#endif
+          }
+        }
+      }
+      if (k + 2 < NCHK) {
+        __syncthreads();  // every wave is done with buffer k & 1
+        rdma(k + 2);
+      }
+    }
+    __syncthreads();  // the chunk buffers become the statistics scratch
+    LNCH_T(3);
+  }
+#else
   {
     // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
     // hoisting all C * CB of them, which would spill the accumulators)
@@ -404,6 +549,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #endif
     }
   }
+#endif
   float* red = reinterpret_cast<float*>(smem);   // [NWV waves][NR][64 lanes] partial sums
   float* tot = red + NWV * NR * 64;               // [EPT][TS] totals (odd stride: 16 banks)
   auto lane_sum = [&](int c) {
@@ -435,6 +581,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const float* mt = tot + l16e * TS;  // this lane's electron
   // channel means, centre
   reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
+  LNCH_T(4);
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const float mu = mt[c];
@@ -477,6 +624,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         return r;
       },
       std::integral_constant<int, NR>{});
+  LNCH_T(5);
   const float s = 1.f / sqrtf(mt[0] + 1e-5f), s2 = s * s;
   float cl = 0.f, au[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -535,13 +683,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  LNCH_T(6);
+  LNCH_RT(9);
 }
 
 template <int N, int NWV>
 void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
                    float* h, int ne, int mode, hipStream_t s) {
-  constexpr int C = 2 * N + 5;
-  const size_t smem = 2ull * 3 * C * LN_EPT * 64 + ((LN_EPT + N - 1) / N + 1) * N * 16;
+  const size_t smem = lnch_smem(N);
   const int grid = (ne + LN_EPT - 1) / LN_EPT;
   if (mode == 0) {
     ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);
@@ -561,6 +710,13 @@ void launch_lnch_n(const float* X, const uint16_t* Wp, int ldp, const float* bia
 }
 
 }  // namespace
+
+#if LNCH_STAMP
+extern "C" int dh_debug_lnch_stamps(unsigned long long* out, int n) {
+  n = n < LNCH_STAMP_WG * LNCH_NSTAMP ? n : LNCH_STAMP_WG * LNCH_NSTAMP;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lnch_stamp), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 bool gemm_lnch_supported(int N, int D) {
   if (D != LN_D || N < 1 || N > 6) return false;

@@ -207,7 +207,16 @@ class LogManager:
             if keys and opt_init is not None:
                 opt_state = opt_init(params)
                 if opt_state is not None:
-                    opt_state.load_state_dict({k.split("/", 1)[1]: f[k] for k in keys})
+                    try:
+                        opt_state.load_state_dict({k.split("/", 1)[1]: f[k] for k in keys})
+                    except (KeyError, ValueError, RuntimeError) as e:
+                        # the optimizer changed since the checkpoint was written (e.g. an Adam
+                        # checkpoint restored into a run with the KFAC default): keep the params,
+                        # walkers and step, start the optimizer state afresh
+                        logger.warning("Checkpoint %s: optimizer state does not match the current optimizer "
+                                       "(%s: %s); params, walkers and step restored, optimizer state "
+                                       "re-initialised", path, type(e).__name__, e)
+                        opt_state = opt_init(params)
             width = float(f["mcmc_width"])
         logger.info("Restored checkpoint %s", path)
         return step, CheckpointState(params, shard, opt_state, width)

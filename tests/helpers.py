@@ -106,7 +106,7 @@ FLOOR_X_MAX_POLE = 6.0  # theta within 0.15 rad of a pole: 1/sin(theta) amplifie
 FLOOR_SLACK = 2e-7   # observables the float32 run happens to get (nearly) exact
 
 
-def within_f32_floor(err_hip, err_f32, floor_abs=0.0, max_x=None):
+def within_f32_floor(err_hip, err_f32, floor_abs=0.0, max_x=None, label=None):
     """The kernels' per-walker errors are at or below the float32 run's error distribution:
     median within FLOOR_X, 90th percentile within FLOOR_X_P90 of the float32 run's, the
     maximum within FLOOR_X_MAX (``max_x`` where given), or everything below ``floor_abs``
@@ -115,7 +115,7 @@ def within_f32_floor(err_hip, err_f32, floor_abs=0.0, max_x=None):
     log = os.environ.get("DH_FLOOR_LOG")
     if log:  # margin survey (tools): the three ratios of every gate evaluation
         with open(log, "a") as fh:
-            fh.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "?"),
+            fh.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "?"), "label": label,
                                  "med": float(np.median(e) / max(np.median(f), 1e-30)),
                                  "p90": float(np.percentile(e, 90) / max(np.percentile(f, 90), 1e-30)),
                                  "max": float(e.max() / max(f.max(), 1e-30)),

@@ -12,6 +12,10 @@ the 8-GPU runs use RCCL), writing argv[1]_<rank>.npz:
   step (save_time_interval 0, save_step_interval 1: the collective save decision),
   the run directory in argv[3]; the final parameters and this rank's walkers.
 * ``nccl``: a world-size-1 "nccl" (RCCL) process group and one all-reduce on the GPU.
+* ``kfac``: the default optimizer across ranks (optimizers/kfac.py:195-241, multi_device):
+  make_loss_fn(ENERGY_GRAD, curvature=True) on fixed walkers (the ONE [gradient | curvature
+  statistics] all-reduce), then two KFAC steps of make_optimizer_step on them; the averaged
+  gradient and statistics, the parameters after each step and the preconditioned gradient.
 """
 
 from __future__ import annotations
@@ -61,6 +65,43 @@ def main_train(out, world, rank, run_dir):
              width=float(state.mcmc_width))
 
 
+def main_kfac(out, world, rank):
+    from deephall_amd import Config, make_network
+    from deephall_amd.loss import LossMode, make_loss_fn
+    from deephall_amd.optimizers import make_optimizer_step
+    from deephall_amd.types import CheckpointState
+    from helpers import make_walkers
+
+    cfg = Config.from_dict({
+        "batch_size": 64, "seed": 42,
+        "system": {"nspins": (3, 0), "flux": 2},
+        "network": {"psiformer": {"num_layers": 2, "num_heads": 2, "heads_dim": 16}},
+        "optim": {"optimizer": "kfac"},
+    })
+    model = make_network(cfg.system, cfg.network)
+    params = model.init(11, device="cuda")
+    B = 64
+    per = B // world
+    x = torch.tensor(make_walkers(B, 3, seed=21)[rank * per : (rank + 1) * per], device="cuda")
+    loss_grad = make_loss_fn(model, cfg.system, LossMode.ENERGY_GRAD, curvature=True)
+    stats, grad = loss_grad(params, x)
+    g0 = grad.flat.clone()
+    curv = loss_grad.curvature.clone()
+    init, step = make_optimizer_step(cfg, model)
+    state = CheckpointState(params, x, init(params), 0.1)
+    p0 = params.flat.clone()
+    snaps, pgs = [], []
+    for _ in range(2):
+        state, _ = step(state)
+        snaps.append(state.params.flat.clone())
+        pgs.append(state.opt_state.pgrad.clone())
+    torch.cuda.synchronize()
+    np.savez(f"{out}_{rank}.npz", grad=g0.cpu().numpy(), curv=curv.cpu().numpy(), p0=p0.cpu().numpy(),
+             p1=snaps[0].cpu().numpy(), p2=snaps[1].cpu().numpy(), pg1=pgs[0].cpu().numpy(),
+             pg2=pgs[1].cpu().numpy(), info=state.opt_state.info.cpu().numpy(),
+             energy=complex(stats["energy"].item()))
+
+
 def main_nccl(out):
     import socket
 
@@ -93,6 +134,8 @@ def main():
         main_grad(out, world, rank)
     elif mode == "train":
         main_train(out, world, rank, sys.argv[3])
+    elif mode == "kfac":
+        main_kfac(out, world, rank)
     else:
         main_vmc(out, world, rank)
     if world > 1:

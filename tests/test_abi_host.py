@@ -209,3 +209,40 @@ def test_dh_config_rejects_foreign_layouts():
     cfg.struct_size = C.sizeof(_lib.DhConfig)
     assert lib.dh_create(C.byref(cfg), C.byref(h)) == 0
     lib.dh_destroy(h)
+
+
+def test_restore_keeps_params_when_optimizer_changed(tmp_path):
+    """An Adam checkpoint (opt_state/mu, nu, count) restored into a run whose optimizer state
+    has other keys (KFAC: raw, weight, step): params, walkers and step come back, the optimizer
+    state is re-initialised with a warning instead of the whole checkpoint being skipped
+    (log.py restore_checkpoint)."""
+    from deephall_amd import config
+    from deephall_amd.log import LogManager
+    from deephall_amd.networks import make_network
+
+    model = make_network(config.System(nspins=(3, 0), flux=2), config.Network())
+    p = model.init(3, device="cpu")
+    arrays = {"step": np.asarray(4), "mcmc_width": np.asarray(0.25), "data": np.zeros((6, 3, 2), np.float32)}
+    for k, v in p.items():
+        arrays[f"params/{k}"] = v.numpy()
+    n = p.flat.numel()
+    arrays.update({"opt_state/mu": np.zeros(n, np.float32), "opt_state/nu": np.zeros(n, np.float32),
+                   "opt_state/count": np.asarray(5)})
+    path = tmp_path / "ckpt_000004.npz"
+    np.savez_compressed(path, **arrays)
+
+    class KfacLike:
+        inits = 0
+
+        def __init__(self):
+            KfacLike.inits += 1
+            self.raw = torch.zeros(3)
+
+        def load_state_dict(self, d):
+            self.raw.copy_(torch.as_tensor(d["raw"]))
+
+    step, st = LogManager.restore_checkpoint(path, model, torch.device("cpu"), lambda params: KfacLike())
+    assert step == 5 and st.mcmc_width == 0.25 and st.data.shape == (6, 3, 2)
+    for k in p:
+        assert torch.equal(st.params[k], p[k])
+    assert isinstance(st.opt_state, KfacLike) and KfacLike.inits == 2

@@ -134,6 +134,34 @@ def test_train_two_ranks_checkpoint(tmp_path):
     assert np.array_equal(res["params"], two[0]["params"])
 
 
+def test_kfac_two_ranks(tmp_path):
+    """KFAC across ranks (kfac_jax multi_device, reference
+    optimizers/kfac.py:214-215): 2 ranks on equal shards of 64 fixed walkers against one rank
+    holding all of them.  The ONE [gradient | curvature statistics] all-reduce gives the
+    one-rank gradient and Fisher statistics (layer Gram matrices, derived attention-output
+    factors, generic diagonal) to f32 rounding; after each of two KFAC steps both ranks hold
+    bit-identical parameters, and the preconditioned gradient P g and the parameters equal
+    the one-rank run's to the f32 rounding of the statistics carried through the damped
+    inverses."""
+    _gpu_or_skip()
+    one = _run_ranks(1, tmp_path / "k1", "kfac")[0]
+    two = _run_ranks(2, tmp_path / "k2", "kfac")
+    for k in ("grad", "curv", "p1", "p2", "pg1", "pg2"):
+        assert np.array_equal(two[0][k], two[1][k]), k  # every rank holds the same values
+    g1, g2 = one["grad"], two[0]["grad"]
+    assert np.all(np.isfinite(g1)) and np.abs(g1).max() > 0
+    assert np.abs(g2 - g1).max() <= 2e-5 * np.abs(g1).max()
+    c1, c2 = one["curv"], two[0]["curv"]
+    assert np.all(np.isfinite(c1)) and np.abs(c1).max() > 0
+    assert np.abs(c2 - c1).max() <= 2e-5 * np.abs(c1).max(), np.abs(c2 - c1).max() / np.abs(c1).max()
+    for s in (1, 2):
+        pg1, pg2 = one[f"pg{s}"], two[0][f"pg{s}"]
+        assert np.abs(pg2 - pg1).max() <= 1e-3 * np.abs(pg1).max(), (s, np.abs(pg2 - pg1).max() / np.abs(pg1).max())
+        d1, d2 = one[f"p{s}"] - one["p0"], two[0][f"p{s}"] - two[0]["p0"]
+        assert np.abs(d1).max() > 0
+        assert np.abs(d2 - d1).max() <= 1e-3 * np.abs(d1).max(), (s, np.abs(d2 - d1).max() / np.abs(d1).max())
+
+
 def test_rccl_process_group():
     """a world-size-1 "nccl" process group (RCCL on ROCm) initialises
     on the box and all-reduces on the GPU; constants.pmean runs through it."""

@@ -30,7 +30,8 @@ from test_gpu_parity import build
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
-CASES = ["C1_pole", "C2_pole", "MIX_pole", "C1_harmonic", "C2_harmonic_radius", "C2_radius", "C2", "C4", "C5"]
+CASES = ["C1_pole", "C2_pole", "MIX_pole", "C1_harmonic", "C2_harmonic_radius", "C2_radius", "C2", "C4", "C5",
+         "C1_sparse", "C2_sparse", "MIX_sparse"]
 OBS = [("e_l", None), ("kinetic", "kinetic"), ("lz", "angular_momentum_z"), ("lz2", "angular_momentum_z_square"),
        ("l2", "angular_momentum_square")]
 
@@ -62,11 +63,11 @@ def test_within_float32_floor(cuda, tag):
     err_lp = rel(lp.real, g["logpsi"].real)
     err_lp32 = rel(g["logpsi32"].real, g["logpsi"].real)
     rows.append(("logpsi", err_lp, err_lp32))
-    if not within_f32_floor(err_lp, err_lp32, 1e-5, max_x):
+    if not within_f32_floor(err_lp, err_lp32, 1e-5, max_x, label=f"{tag}/logpsi"):
         fails.append("logpsi")
     dphi = np.abs(np.angle(np.exp(1j * (lp.imag - g["logpsi"].imag))))
     dphi32 = np.abs(np.angle(np.exp(1j * (g["logpsi32"].imag - g["logpsi"].imag))))
-    if not within_f32_floor(dphi, dphi32, 1e-5, max_x):
+    if not within_f32_floor(dphi, dphi32, 1e-5, max_x, label=f"{tag}/phase"):
         fails.append("phase")
     if not rel(got["potential"], g["potential"]).max() < 1e-5:
         fails.append("potential")
@@ -74,7 +75,7 @@ def test_within_float32_floor(cuda, tag):
         ref, r32 = g[key], g[key + "32"]
         eh, e32 = rel(got[key], ref), rel(r32, ref)
         rows.append((key, eh, e32))
-        if not within_f32_floor(eh, e32, 0.0, max_x):
+        if not within_f32_floor(eh, e32, 0.0, max_x, label=f"{tag}/{key}"):
             fails.append(key)
     rows.insert(1, ("phase", dphi, dphi32))
     print(f"\n{tag}: observable | HIP max p90 median | float32 run max p90 median  (relative, floor 1)")

@@ -85,6 +85,46 @@ def test_kfac_statistics_match_oracle(cuda, name, B, layers):
     assert gerr < 1e-4
 
 
+def test_kfac_vjp_with_cotangent_and_chunks(cuda):
+    """The training path of dh_kfac_vjp: a real cotangent (the gradient's and the
+    Fisher pass share one saved forward) and walker chunks (the statistics accumulated across
+    chunks, api.cpp's kf.acc).  The statistics equal the ct=None single-chunk result, the
+    returned gradient equals model.vjp's, and the chunked run equals the unchunked one."""
+    from deephall_amd.networks import psiformer as pf
+
+    ocfg = oracle_config("C1", num_layers=2)
+    p64 = make_params(ocfg)
+    system, model = build(ocfg)
+    params = to_device_params(p64)
+    B = 24
+    x = torch.tensor(make_walkers(B, ocfg.nelec, seed=33), device=cuda)
+    ct = torch.tensor(np.random.default_rng(5).standard_normal((B, 2)), dtype=torch.float32, device=cuda)
+    lay = _slots(model, cuda)
+    s_ref = torch.full((lay["nstats"],), float("nan"), device=cuda)
+    model.kfac_vjp(params, x, None, None, s_ref)
+    g_ref = model.vjp(params, x, ct).flat.clone()
+    s_ct = torch.full_like(s_ref, float("nan"))
+    g_ct = ParamTree.zeros(model.spec, cuda)
+    model.kfac_vjp(params, x, ct, g_ct, s_ct)
+    h = model.prepare(params, x.device)
+    old = pf.VJP_WORKSPACE_BYTES
+    try:
+        pf.VJP_WORKSPACE_BYTES = h.lib.dh_kfac_workspace_bytes(h.h, 7)  # chunks of <= 7 walkers
+        s_ch = torch.full_like(s_ref, float("nan"))
+        g_ch = ParamTree.zeros(model.spec, cuda)
+        model.kfac_vjp(params, x, ct, g_ch, s_ch)
+    finally:
+        pf.VJP_WORKSPACE_BYTES = old
+    torch.cuda.synchronize()
+    smax = s_ref.abs().max().item()
+    gmax = g_ref.abs().max().item()
+    assert torch.isfinite(s_ct).all() and torch.isfinite(s_ch).all()
+    assert (s_ct - s_ref).abs().max().item() <= 1e-6 * smax
+    assert (g_ct.flat - g_ref).abs().max().item() <= 1e-6 * gmax
+    assert (s_ch - s_ref).abs().max().item() <= 2e-6 * smax, (s_ch - s_ref).abs().max().item() / smax
+    assert (g_ch.flat - g_ref).abs().max().item() <= 2e-6 * gmax
+
+
 def test_kfac_step_matches_oracle(cuda):
     ocfg = oracle_config("C1", num_layers=2)
     p64 = make_params(ocfg)

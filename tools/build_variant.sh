@@ -1,0 +1,16 @@
+#!/bin/bash
+# A/B builds of one source file: compile csrc/$FILE with extra -D flags and link it with the
+# in-tree objects of every other file into ab/$NAME.so (timed on the GPU box through
+# DH_LIB_PATH=ab/$NAME.so).  Usage: FILE=gemm_lnch.hip bash tools/build_variant.sh NAME "-DX=1 ..."
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; FLAGS=$2; FILE=${FILE:-gemm_lnch.hip}
+python -c "from deephall_amd import _build; _build.build()" > /dev/null
+mkdir -p ab build/ab
+OBJ=build/ab/$NAME.$FILE.o
+EXTRA=""; [ "$FILE" = "gemm_x6.hip" ] && EXTRA="-fno-slp-vectorize"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I include $EXTRA $FLAGS \
+  -c deephall_amd/csrc/$FILE -o $OBJ
+OBJS=$(ls build/gfx950/*.o | grep -v "/$FILE.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$NAME.so $OBJS $OBJ
+echo "built ab/$NAME.so ($FLAGS)"

@@ -13,7 +13,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from deephall_amd import hamiltonian  # noqa: E402
-from helpers import make_params, to_device_params  # noqa: E402
+from helpers import cancellation_scales, make_params, to_device_params  # noqa: E402
 from oracle import reference as R  # noqa: E402
 from test_gpu_parity import build  # noqa: E402
 
@@ -35,3 +35,17 @@ for k in got:
     print(f"{k:8s} HIP max {eh.max():.2e} p90 {np.percentile(eh, 90):.2e} med {np.median(eh):.2e} | "
           f"f32 max {e32.max():.2e} p90 {np.percentile(e32, 90):.2e} | worst {worst.tolist()} "
           f"{np.round(eh[worst] / np.maximum(e32[worst], 1e-12), 1).tolist()} x f32", flush=True)
+
+# the worst walkers against the size of the terms that cancel in each observable (float64
+# channel oracle): an error that is eps_f32 x that scale is the f32 floor of the walker
+p64 = make_params(ocfg, seed=int(g["param_seed"]))
+sc = cancellation_scales(p64, ocfg, g["x"])
+for k, key in (("kinetic", "kinetic"), ("lz2", "angular_momentum_z_square"), ("l2", "angular_momentum_square"),
+               ("lz", "angular_momentum_z")):
+    ref, r32 = g[k], g[k + "32"]
+    ah, a32 = np.abs(got[k] - ref), np.abs(r32 - ref)
+    s = np.maximum(sc[key], 1.0)
+    worst = np.argsort(ah / np.maximum(np.abs(ref), 1.0))[-3:][::-1]
+    print(f"{k:8s} err/scale HIP max {np.max(ah / s):.2e} med {np.median(ah / s):.2e} | f32 max {np.max(a32 / s):.2e} "
+          f"med {np.median(a32 / s):.2e} | worst walkers {worst.tolist()} |ref| {np.abs(ref[worst]).round(3).tolist()} "
+          f"scale {s[worst].round(1).tolist()} HIP {ah[worst].tolist()} f32 {a32[worst].tolist()}", flush=True)

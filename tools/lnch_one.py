@@ -39,3 +39,18 @@ for i in range(reps + 1):
 torch.cuda.synchronize()
 ts = [ev[2 * i].elapsed_time(ev[2 * i + 1]) * 1e3 for i in range(reps)]
 print(f"gemm_lnch N={N} B={B} mode={mode}: {sum(ts) / len(ts):.1f} us per launch (min {min(ts):.1f})")
+if hasattr(lib, "dh_debug_lnch_stamps"):  # LNCH_STAMP=1 diagnostic build: phase breakdown of the last launch
+    import numpy as np
+
+    nwg = min((ne + 15) // 16, 4096)
+    buf = (C.c_ulonglong * (4096 * 10))()
+    assert lib.dh_debug_lnch_stamps(buf, 4096 * 10) == 0
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 10)[:nwg].astype(np.float64)
+    clk = (st[:, 6] - st[:, 0]) / ((st[:, 9] - st[:, 8]) / 100e6)  # shader clock, Hz
+    f = np.median(clk)
+    names = ["prologue", "k loop", "residual", "reduce 1", "reduce 2", "LN + stores"]
+    d = np.diff(st[:, :7], axis=1) / f * 1e6
+    print(f"stamps: clock {f / 1e9:.2f} GHz, {nwg} workgroups, per-WG span {np.median((st[:, 6] - st[:, 0]) / f * 1e6):.1f} us "
+          f"(launch span {(st[:, 9].max() - st[:, 8].min()) / 100:.1f} us)")
+    for i, n in enumerate(names):
+        print(f"  {n:12s} median {np.median(d[:, i]):7.2f} us  p90 {np.percentile(d[:, i], 90):7.2f}")
