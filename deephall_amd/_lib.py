@@ -60,6 +60,7 @@ EXPORTS = [
     "dh_debug_gemm_x6_ln",
     "dh_debug_chain_x6",
     "dh_debug_gemm_lnch",
+    "dh_debug_set_lnch_form",
     "dh_debug_x6_plane_rows",
     "dh_debug_split_planes",
     "dh_debug_gemm_x6",
@@ -171,6 +172,8 @@ def load(path: Path | str | None = None):
     lib.dh_debug_chain_x6.restype = i32
     lib.dh_debug_gemm_lnch.argtypes = [i32, i32, vp, vp, i32, vp, vp, vp, vp, i32, vp]
     lib.dh_debug_gemm_lnch.restype = i32
+    lib.dh_debug_set_lnch_form.argtypes = [i32]
+    lib.dh_debug_set_lnch_form.restype = i32
     lib.dh_debug_x6_plane_rows.argtypes = [i32]
     lib.dh_debug_x6_plane_rows.restype = i32
     lib.dh_debug_split_planes.argtypes = [vp, i32, i32, i32, vp, vp]

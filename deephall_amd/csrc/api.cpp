@@ -102,6 +102,7 @@ struct KfacHost {
   int s_feat = -1, s_h0 = -1;
   KfacLayerSlots lay[16];
   int A_orb[2] = {-1, -1}, G_orb[2][2] = {{-1, -1}, {-1, -1}};
+  int A_lll = -1, G_lll = -1;  // "sparse" orbitals: the complex lll_weight block
   struct Blk {
     int kseg, bseg, din, dout, a, g;
     float scale;
@@ -890,6 +891,7 @@ struct GradWork {
   float *P, *dWol, *dbol;                                     // chunk partials, folded-weight grads
   float *dWorb, *dborb;                                       // full-layout orbital grads ("sparse")
   float *fgrad, *ctf;                                         // KFAC: Fisher tangent (ref layout), cotangent
+  float *kfs0, *kfs1;                                         // KFAC "sparse": featured-orbital rows
   size_t total_bytes;
 };
 
@@ -925,7 +927,11 @@ GradWork carve_grad(const Dims& d, int nw, void* base, size_t nref = 0) {
   const size_t nch = (size_t)grad_chunks(rows);
   const size_t MNK = (size_t)d.M * d.N * d.K;
   // (KFAC: the orbital output Gram matrices need MNK^2 per chunk)
-  const size_t pw = std::max({D * 3 * D, D * (size_t)d.ld_orb, (size_t)4 * D, nref ? MNK * MNK : (size_t)0});
+  // ("sparse" KFAC: the featured-orbital tangent Gram (8 N K)^2, the lll_weight factors over
+  //  N K times as many rows: 64 and M^2 per chunk of those)
+  const size_t F8 = (size_t)8 * d.N * d.K, pls = (nref && d.sparse) ? std::max(F8 * F8, (size_t)d.N * d.K *
+                                                                       std::max<size_t>(64, (size_t)d.M * d.M)) : 0;
+  const size_t pw = std::max({D * 3 * D, D * (size_t)d.ld_orb, (size_t)4 * D, nref ? MNK * MNK : (size_t)0, pls});
   const size_t pc = std::max((size_t)3 * D, (size_t)d.ld_orb);
   w.P = take(std::max({nch * pw, nch * pc, (size_t)ln_bwd_blocks(rows) * 2 * D, (size_t)nw * 2}));
   w.dWol = take(D * D);
@@ -937,6 +943,10 @@ GradWork carve_grad(const Dims& d, int nw, void* base, size_t nref = 0) {
   if (nref) {
     w.fgrad = take(nref);
     w.ctf = take((size_t)nw * 2);
+    if (d.sparse) {
+      w.kfs0 = take(rp * 8 * d.N * d.K);
+      w.kfs1 = take(rp * 8 * d.N * d.K);
+    }
   }
   w.total_bytes = off * sizeof(float);
   return w;
@@ -1042,18 +1052,47 @@ int vjp_backward(dh_handle* h, const float* x, int nw, const float* ct, float* g
     const int MNK = d.M * d.N * d.K;
     if (fisher) {
       const KfacHost& K = *kf->plan;
+      const int NK = d.N * d.K, F8 = 8 * NK;
+      const float inv_lll = kf->inv_rows / (float)NK;  // rows of the lll block: B N N K
       int lo = 0;
       for (int a = 0, blk = 0; a < 2; ++a) {
         const int na = a == 0 ? d.n_up : d.n_dn;
         if (na == 0) continue;
-        for (int part = 0; part < 2; ++part)
-          gram(w.dF + (size_t)(blk * 2 + part) * MNK, d.ld_orb, MNK, K.G_orb[blk][part], kf->inv_rows_blk[blk], rows,
-               false);
-        if (d.NB == 1) {
-          gram(w.hs[d.L], D, D, K.A_orb[blk], kf->inv_rows_blk[blk], rows, true);
-        } else {  // this spin block's rows of every walker, gathered
+        const int nr = d.NB == 1 ? rows : nw * na;
+        if (!d.sparse)
+          for (int part = 0; part < 2; ++part)
+            gram(w.dF + (size_t)(blk * 2 + part) * MNK, d.ld_orb, MNK, K.G_orb[blk][part], kf->inv_rows_blk[blk],
+                 rows, false);
+        const float* hb = w.hs[d.L];
+        if (d.NB > 1) {  // this spin block's rows of every walker, gathered
           launch_copy2d(w.hs[d.L] + (size_t)lo * D, d.N * D, w.dqkv, na * D, nw, na * D, s);
-          gram(w.dqkv, D, D, K.A_orb[blk], kf->inv_rows_blk[blk], nw * na, true);
+          hb = w.dqkv;
+        }
+        gram(hb, D, D, K.A_orb[blk], kf->inv_rows_blk[blk], nr, true);
+        if (d.sparse) {
+          const int nlo = d.NB == 1 ? 0 : lo, nna = d.NB == 1 ? d.N : na;
+          // featured-orbital tangents (lll dF) -> the DenseGeneral G factors
+          for (int part = 0; part < 2; ++part) {
+            launch_kfac_sparse_dphi(w.dF, d.ld_orb, ref(RS.lll(0)), d.M, NK, blk * 2 + part, nr, nna, d.N, nlo,
+                                    w.kfs0, s);
+            gram(w.kfs0, F8, F8, K.G_orb[blk][part], kf->inv_rows_blk[blk], nr, false);
+          }
+          // the lll_weight input (the real featured orbitals h W + b, exact f32) in rows of 8,
+          // its output tangent (the real feature segment) in rows of M; spin blocks accumulate
+          KfacAcc k2 = *kf;
+          k2.acc = kf->acc || blk > 0;
+          launch_gemm(hb, D, ref(RS.orb_kernel(2 * blk)), F8, ref(RS.orb_bias(2 * blk)), nullptr, 0, w.kfs1, F8, nr,
+                      F8, D, 1, s);
+          const KfacAcc* keep = kf;
+          kf = &k2;
+          gram(w.kfs1, 8, 8, K.A_lll, inv_lll, nr * NK, false);
+          launch_kfac_sparse_regroup(w.dF, d.ld_orb, d.M, NK, blk * 2, nr, nna, d.N, nlo, w.F, s);
+          gram(w.F, d.M, d.M, K.G_lll, inv_lll, nr * NK, false);
+          kf = keep;
+          // the generic lll bias tangent: sum over rows of the real feature segment
+          launch_colsum_partial(w.F, d.M, nr * NK, d.M, w.P, s);
+          launch_reduce2d(w.P, grad_chunks(nr * NK), (size_t)d.M, d.M, 1, d.M, g(RS.lll(1)), d.M, 1.f, acc || blk > 0,
+                          s);
         }
         lo += na;
         ++blk;
@@ -1169,7 +1208,6 @@ int run_vjp(dh_handle* h, const float* x, int nw, const float* ct, float* grad, 
 int kfac_plan(dh_handle* h) {
   if (h->kfac) return DH_OK;
   const Dims& d = h->d;
-  if (d.sparse) return fail(DH_EINVAL, "KFAC: sparse orbitals are not supported (use orbital 'full')");
   if (d.L > 16) return fail(DH_EINVAL, "KFAC: too many layers");
   auto* K = new KfacHost();
   const int D = d.D, N = d.N, MNK = d.M * d.N * d.K;
@@ -1204,15 +1242,24 @@ int kfac_plan(dh_handle* h) {
     blk(RS.lay(l, RWl), -1, D, D, L.A_Wl, L.G_T, (float)N);
     blk(RS.lay(l, RWm), RS.lay(l, Rbm), D, D, L.A_h1, L.G_z, (float)N);
   }
+  // featured orbitals: M N K outputs, or 8 N K for "sparse" (then mixed by lll_weight)
+  const int FNK = d.sparse ? 8 * N * d.K : MNK;
   for (int a = 0, b = 0; a < 2; ++a) {
     const int na = a == 0 ? d.n_up : d.n_dn;
     if (na == 0) continue;
     K->A_orb[b] = slot(D + 1);
     for (int part = 0; part < 2; ++part) {
-      K->G_orb[b][part] = slot(MNK);
-      blk(RS.orb_kernel(2 * b + part), RS.orb_bias(2 * b + part), D, MNK, K->A_orb[b], K->G_orb[b][part], (float)na);
+      K->G_orb[b][part] = slot(FNK);
+      blk(RS.orb_kernel(2 * b + part), RS.orb_bias(2 * b + part), D, FNK, K->A_orb[b], K->G_orb[b][part], (float)na);
     }
     ++b;
+  }
+  if (d.sparse) {
+    // lll_weight: kfac.py's repeated_dense_complex_no_bias block, its statistics as
+    // RepeatedDenseBlock computes them (inputs regrouped into rows of 8, scale 8 N^2)
+    K->A_lll = slot(8);
+    K->G_lll = slot(d.M);
+    blk(RS.lll(0), -1, 8, d.M, K->A_lll, K->G_lll, (float)(8 * N * N));
   }
   // generic (diagonal) parameters: LayerNorm scale / bias, Jastrow alphas
   KfacGenTable& G = K->dev.gen;
@@ -1225,6 +1272,7 @@ int kfac_plan(dh_handle* h) {
   };
   for (int l = 0; l < d.L; ++l)
     for (int k : {Rln1s, Rln1b, Rln2s, Rln2b}) gen(RS.lay(l, k), D);
+  if (d.sparse) gen(RS.lll(1), d.M);  // lll_weight's bias: no pattern covers it
   gen(RS.jas(0), 1);
   gen(RS.jas(1), 1);
   K->nstats = K->nmat + (size_t)G.total;
@@ -1554,6 +1602,9 @@ int dh_debug_gemm_lnch(int N, int mode, const float* X, const uint16_t* Wp, int 
   launch_gemm_lnch(N, mode == 0 ? X : h, Wp, ldp, bias, ln, geo, h, ne, mode, (hipStream_t)stream);
   return check_launch();
 }
+
+// which fused channel-tail kernel the local energy uses (DH_LNCH at start-up): tests only
+int dh_debug_set_lnch_form(int form) { return set_lnch_form(form); }
 
 int dh_debug_gemm_ln(int mode, int bm, const float* X, int ldx, const float* Wt, int ldw, const float* bias,
                      const float* ln, float* h, int rows, int K, void* stream) {

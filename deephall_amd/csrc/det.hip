@@ -49,10 +49,18 @@ struct FView {
 struct EnvLeaf {
   cf e0, dth, dph, lb, d2th;
 };
-// `gauge` = sigma * Q removes the per-electron phase exp(i sigma Q phi) from the envelope
-// (north patch sigma = +1, south patch sigma = -1; 0 = reference gauge).  The network
-// channels then stay regular near the poles; the removed term i Q sum sigma phi is
-// added back analytically (in double) by the energy assembly.
+// `gauge` = kappa removes the per-electron phase exp(i kappa phi) from the envelope (0 =
+// reference gauge); the removed term i sum_i kappa_i phi_i is added back analytically (in
+// double) by the energy assembly.  kappa_i = env_gauge(cos theta_i): the envelope's dominant
+// harmonic m* = Q cos theta (|u|^2 = cos^2 theta/2 weights Q + m binomially), so the phi
+// derivatives i (m - kappa) of the contracted orbitals stay small for every electron.  At the
+// poles this is the north / south patch (kappa = +-Q: regular channels where the reference's
+// 1 / sin theta terms blow up); near the equator it stays ~0 where the patch choice put up to
+// 2Q into every phi channel and the f32 contractions below lost the digits.
+// Quantised to 1/64 of Q so that m - kappa is exact in f32.
+__device__ __forceinline__ float env_gauge(float ct, int M) {
+  return (float)(M - 1) * __builtin_rintf(64.f * ct) * (1.f / 128.f);
+}
 __device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm, bool leaves, float gauge = 0.f,
                                    bool sq = false) {
   const int a = p, b = M - 1 - p;
@@ -419,7 +427,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   for (int c = 0; c < RING - 1 && c < C; ++c) issue(c, 0);
   {
     const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
-    const float gauge = ct >= 0.f ? Q : -Q;
+    const float gauge = env_gauge(ct, M);
     const float phh[3] = {-sp, cp, 0.f};
     const float thh[3] = {ct * cp, ct * sp, -st};
 #pragma unroll
@@ -726,7 +734,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
   }
   for (int idx = tid; idx < (PC ? 0 : N * M); idx += nt) {
     const int i = idx / M, p = idx % M;
-    const float gauge = (geo[4 * i + 1] >= 0.f ? Q : -Q);
+    const float gauge = env_gauge(geo[4 * i + 1], M);
     const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true, gauge);
     E0[idx] = e.e0;
     DTH[idx] = e.dth;
@@ -889,7 +897,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
           acc = phic(kd, 2 + T + k, idx);  // includes 2 Gu_k
         } else {
           for (int p = 0; p < M; ++p) {
-            const float m = (float)p - 0.5f * (float)(M - 1) - (ct >= 0.f ? Q : -Q);
+            const float m = (float)p - 0.5f * (float)(M - 1) - env_gauge(ct, M);
             const cf sf = env_flow2(E0[i * M + p], DTH[i * M + p], D2[i * M + p], m, st, ct, sp, cp, k);
             cfma(acc, STAGED ? fs(Fc, i, p, j, kd) : F.at(r0 + 2 + T + k, blk, p, j, kd), E0[i * M + p]);
             cfma(acc, STAGED ? fs(Fv, i, p, j, kd) : F.at(r0, blk, p, j, kd), sf);
@@ -969,8 +977,8 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
       (void)jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
       jg += (-f1 / r) * (rj[0] * et[0] + rj[1] * et[1] + rj[2] * et[2]);
     }
-    // gauge term A = i Q sum_i sigma_i phi_i (env_leaf) on the phi tangent
-    if (t & 1) gi += Q * ((geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0) / sti;  // the leaves' patch choice
+    // gauge term A = i sum_i kappa_i phi_i (env_leaf) on the phi tangent
+    if (t & 1) gi += (double)env_gauge(geo[4 * i + 1], M) / sti;  // the leaves' kappa
     tgr[t] = gr + jg;
     tgi[t] = gi;
   } else if (tid < T + N) {
@@ -1044,15 +1052,15 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
     double gauge_phase = 0.0;
     for (int i = 0; i < N; ++i) {
       const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
-      const double sg = (geo[4 * i + 1] >= 0.f) ? 1.0 : -1.0;  // the leaves' patch choice
-      gauge_phase += Q * sg * (double)x[2 * (b * N + i) + 1];
+      const double kap = (double)env_gauge(geo[4 * i + 1], M);  // the leaves' kappa
+      gauge_phase += kap * (double)x[2 * (b * N + i) + 1];
       const double cot = ct / st;
       const double tdot[3] = {-sp, cp, 0.0};
       const double thp[3] = {cp * cot, sp * cot, -1.0};
       const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
       const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
 #pragma unroll
-      for (int kk = 0; kk < 3; ++kk) S_im[kk] += Q * sg * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
+      for (int kk = 0; kk < 3; ++kk) S_im[kk] += kap * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
     }
     pe *= (double)lambda;
     LB_re += Jlb;

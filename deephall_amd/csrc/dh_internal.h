@@ -119,6 +119,12 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 // in place over h [ne * C][256]; X [ne * C][256] (mode 1: X = h); split-bf16 arithmetic.
 // DH_LNCH=0 selects the GEMM + layernorm_ch pair instead.
 bool gemm_lnch_supported(int N, int D);
+int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel, 2 gemm_lnch2_kernel; returns the previous form
+// gemm_lnch2.hip: the same operation on 16 / S-electron tiles (S channel classes), two
+// workgroups per CU, N <= 12 and 16, 20, 24
+bool gemm_lnch2_supported(int N);
+void launch_gemm_lnch2(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
+                       const float* geo, float* h, int ne, int mode, hipStream_t s);
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s);
 bool chain_x6_enabled();
@@ -295,6 +301,11 @@ struct KfacDevPlan {  // device copies of the job tables (owned by the handle)
 void launch_kfac_aug(const float* P, int nch, int n, float* out, int ld, float scale, float corner, int acc,
                      hipStream_t s);
 void launch_kfac_feat_gram(const Dims& d, const float* geo, int rows, float* P, hipStream_t s);
+// "sparse" orbitals: the featured-orbital tangent lll dF and the lll output tangent as rows of M
+void launch_kfac_sparse_dphi(const float* dF, int ld, const float* lll, int M, int NK, int seg, int nr, int na, int N,
+                             int lo, float* out, hipStream_t s);
+void launch_kfac_sparse_regroup(const float* dF, int ld, int M, int NK, int seg, int nr, int na, int N, int lo,
+                                float* out, hipStream_t s);
 void launch_kfac_fisher_ct(const float* logpsi, int nw, float* ct, hipStream_t s);
 void launch_kfac_generic(const float* fgrad, const KfacGenTable& tab, float* diag, float scale, hipStream_t s);
 void launch_kfac_ema(float* raw, const float* st, size_t n, float ema, hipStream_t s);

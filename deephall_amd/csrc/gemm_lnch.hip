@@ -67,6 +67,9 @@
 #ifndef LNCH_RDMA_LATE
 #define LNCH_RDMA_LATE 1
 #endif
+#ifndef LNCH_PERMLANE  // round-3 variant kept for the electron-slot study: the
+#define LNCH_PERMLANE 0  // four lane rows' partials summed by permlane32/16 swaps, not in LDS
+#endif
 #ifndef LNCH_STAMP
 #define LNCH_STAMP 0
 #endif
@@ -123,6 +126,17 @@ __device__ __forceinline__ uint32_t pkbf(float x, float y) {
 __device__ __forceinline__ float lo_of(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_of(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ int lnch_sw(int e) { return (0x78 >> (2 * ((e >> 2) & 3))) & 3; }
+#if LNCH_PERMLANE
+// sum over the four lanes e, e + 16, e + 32, e + 48 (the round-3 permlane form)
+__device__ __forceinline__ float lnch_sum4g(float v) {
+  const int x = __float_as_int(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  v = __int_as_float(a[0]) + __int_as_float(a[1]);
+  const int y = __float_as_int(v);
+  const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);
+  return __int_as_float(b[0]) + __int_as_float(b[1]);
+}
+#endif
 
 template <int N, int MODE, int NWV>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >= 8 ? 2 : 1, NWV >= 8 ? 2 : 1))) void gemm_lnch_kernel(const float* X, const uint16_t* __restrict__ Wp, int ldp,
@@ -563,7 +577,12 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     constexpr int NS = decltype(NS_)::value;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
+#if LNCH_PERMLANE
+      const float v = lnch_sum4g(part(j));
+      if (kge == 0) red[(wid * NS + j) * 64 + l16e] = v;
+#else
       red[(wid * NS + j) * 64 + lane_e] = part(j);  // every lane's 8-feature partial (no cross-lane ops)
+#endif
       __builtin_amdgcn_sched_barrier(0);          // one statistic at a time (register pressure)
     }
     __syncthreads();
@@ -573,7 +592,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
       for (int w = 0; w < NWV; ++w)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
+        for (int g = 0; g < (LNCH_PERMLANE ? 1 : 4); ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
       tot[e * TS + j] = s * (1.f / D);
     }
     __syncthreads();
@@ -718,18 +737,35 @@ extern "C" int dh_debug_lnch_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-bool gemm_lnch_supported(int N, int D) {
-  if (D != LN_D || N < 1 || N > 6) return false;
-  static int env = -1;
-  if (env < 0) {
+// DH_LNCH: 0 = off (GEMM + layernorm_ch), 1 = gemm_lnch_kernel (16-electron tiles, one per CU),
+// 2 = gemm_lnch2_kernel (8-electron tiles, two per CU: gemm_lnch2.hip)
+static int g_lnch_form = -1;  // -1: not read yet (dh_debug_set_lnch_form overrides it)
+static int lnch_form() {
+  if (g_lnch_form < 0) {
     const char* v = getenv("DH_LNCH");
-    env = (v && v[0] == '0') ? 0 : 1;
+    g_lnch_form = (v && v[0] == '0') ? 0 : (v && v[0] == '2') ? 2 : 1;
   }
-  return env != 0;
+  return g_lnch_form;
+}
+
+int set_lnch_form(int f) {
+  const int old = lnch_form();
+  if (f >= 0 && f <= 2) g_lnch_form = f;
+  return old;
+}
+
+bool gemm_lnch_supported(int N, int D) {
+  if (D != LN_D || N < 1) return false;
+  const int f = lnch_form();
+  return f == 1 ? N <= 6 : f == 2 ? gemm_lnch2_supported(N) : false;
 }
 
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s) {
+  if (lnch_form() == 2) {
+    launch_gemm_lnch2(N, X, Wp, ldp, bias, ln, geo, h, ne, mode, s);
+    return;
+  }
   switch (N) {
     case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
     case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;

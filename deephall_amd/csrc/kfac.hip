@@ -334,7 +334,57 @@ __global__ __launch_bounds__(256) void kfac_update_kernel(float* __restrict__ p,
   }
 }
 
+// ---- "sparse" orbitals (oracle/kfac.py header): the rows of spin block
+// [lo, lo + na) of every walker, r = w * na + i -> full row w * N + lo + i.
+__device__ __forceinline__ size_t sparse_row(int r, int na, int N, int lo) {
+  return (size_t)(r / na) * N + lo + (r % na);
+}
+
+// tangent of the featured orbitals (the lll_weight input): out[r][a NK + jk] =
+// sum_m lll[a][m] dF[row(r)][(seg M + m) NK + jk]   (seg = 2 blk + part of the full layout)
+__global__ __launch_bounds__(256) void kfac_sparse_dphi_kernel(const float* __restrict__ dF, int ld,
+                                                               const float* __restrict__ lll, int M, int NK, int seg,
+                                                               int nr, int na, int N, int lo, float* __restrict__ out) {
+  const size_t n = (size_t)nr * 8 * NK;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const int r = (int)(i / (8 * NK)), c = (int)(i % (8 * NK));
+    const int a = c / NK, jk = c % NK;
+    const float* src = dF + sparse_row(r, na, N, lo) * ld + (size_t)seg * M * NK + jk;
+    double acc = 0.0;
+    for (int m = 0; m < M; ++m) acc += (double)lll[a * M + m] * (double)src[(size_t)m * NK];
+    out[i] = (float)acc;
+  }
+}
+
+// the lll_weight output tangent (real part = the real feature segment seg) as rows of M:
+// out[(r NK + jk) M + m] = dF[row(r)][(seg M + m) NK + jk]
+__global__ __launch_bounds__(256) void kfac_sparse_regroup_kernel(const float* __restrict__ dF, int ld, int M, int NK,
+                                                                  int seg, int nr, int na, int N, int lo,
+                                                                  float* __restrict__ out) {
+  const size_t n = (size_t)nr * NK * M;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const int m = (int)(i % M);
+    const size_t q = i / M;
+    const int r = (int)(q / NK), jk = (int)(q % NK);
+    out[i] = dF[sparse_row(r, na, N, lo) * ld + ((size_t)seg * M + m) * NK + jk];
+  }
+}
+
 }  // namespace
+
+void launch_kfac_sparse_dphi(const float* dF, int ld, const float* lll, int M, int NK, int seg, int nr, int na, int N,
+                             int lo, float* out, hipStream_t s) {
+  const size_t n = (size_t)nr * 8 * NK;
+  hipLaunchKernelGGL(kfac_sparse_dphi_kernel, dim3((unsigned)std::min<size_t>(4096, (n + 255) / 256)), dim3(256), 0, s,
+                     dF, ld, lll, M, NK, seg, nr, na, N, lo, out);
+}
+
+void launch_kfac_sparse_regroup(const float* dF, int ld, int M, int NK, int seg, int nr, int na, int N, int lo,
+                                float* out, hipStream_t s) {
+  const size_t n = (size_t)nr * NK * M;
+  hipLaunchKernelGGL(kfac_sparse_regroup_kernel, dim3((unsigned)std::min<size_t>(4096, (n + 255) / 256)), dim3(256), 0,
+                     s, dF, ld, M, NK, seg, nr, na, N, lo, out);
+}
 
 void launch_kfac_aug(const float* P, int nch, int n, float* out, int ld, float scale, float corner, int acc,
                      hipStream_t s) {

@@ -193,8 +193,11 @@ def attention_ch(Qc, Kc, Vc, alpha):
 
 
 def gauge_sign(x):
-    """North (+1) / south (-1) patch of each electron: the gauge the kernels use."""
-    return torch.where(torch.cos(x[..., 0]) >= 0, 1.0, -1.0).to(x.dtype)
+    """kappa_i / Q of each electron's gauge exp(-i kappa_i phi_i): kappa_i = Q cos(theta_i)
+    rounded to 1/64 of Q, the envelope's dominant harmonic (det.hip env_gauge: +-Q at the
+    poles, ~0 on the equator).  Any per-electron constant is exact; this one keeps the phi
+    derivatives of the contracted orbitals small."""
+    return torch.round(64 * torch.cos(x[..., 0])) / 64
 
 
 def envelope_channels(x, Q, gauge=False):
@@ -210,7 +213,7 @@ def envelope_channels(x, Q, gauge=False):
     a = torch.arange(M, dtype=x.dtype)  # Q+m
     b = (M - 1) - a  # Q-m
     m = a - Q
-    if gauge:  # env * exp(-i sigma Q phi): regular near the electron's own pole
+    if gauge:  # env * exp(-i kappa phi), kappa = Q gauge_sign(x)
         m = m - (gauge_sign(x) * Q)[..., None]
     norm = torch.tensor(np.sqrt(ss.comb(2 * Q, Q - np.arange(-Q, Q + 1))), dtype=x.dtype)
     c = torch.cos(th / 2)[..., None]

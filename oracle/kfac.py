@@ -47,7 +47,20 @@ for exactly that configuration.  PARITY UNPINNED beyond the reference's own trai
   c = min(1, sqrt(norm_constraint / (lr^2 <P g, g>))) (kfac_jax's norm constraint on the
   preconditioned gradient), lr = schedule(step), step counting from 0.
 
-Sparse orbitals (blocks.py:52-62, lll_weight on complex features) are not covered.
+* Sparse orbitals (blocks.py:52-62).  The featured DenseGeneral_i then have 8 N K outputs
+  (dense blocks as above).  lll_weight, DenseGeneral(2Q+1, axis=1) applied to the complex
+  featured orbitals x [N, 8, N, K] per walker, is the "repeated_dense_complex_no_bias"
+  pattern (kfac.py:127-133, 175-181) — a RepeatedDenseBlock without bias — and its bias,
+  which that pattern leaves out, is generic.  The block's statistics follow
+  RepeatedDenseBlock.update_curvature_matrix_estimate (kfac.py:78-102) literally:
+  rows = x.size // 8, A from x.real.reshape((rows, -1)) — a row-major regrouping of each
+  walker's [N, 8, N, K] array into consecutive groups of 8 (the contracted axis is axis 1,
+  not the last one, so a group mixes (a, j, k) entries unless N K = 1) — and G from
+  dy.real.reshape((rows, -1)) of the output tangent [N, N, K, M] (dy.real = the tangent with
+  respect to the real part of the output); fixed_scale = prod(x_shape) // (x_shape[0] *
+  x_shape[-1]) = 8 N^2 for x_shape [B, N, 8, N, K].  Whether kfac_jax's graph matcher tags
+  an axis-1 dot_general with this pattern cannot be checked here (kfac_jax is absent);
+  this restatement assumes it does, as the reference's pattern list intends.
 """
 
 from __future__ import annotations
@@ -74,6 +87,7 @@ class Block:
     din: int  # rows of the kernel reshaped [din, dout] (without the bias row)
     dout: int
     scale: float
+    lll: bool = False  # the complex lll_weight block (regrouped inputs / tangents, see header)
 
     @property
     def dA(self):
@@ -82,8 +96,6 @@ class Block:
 
 def blocks(cfg: R.OracleConfig):
     """Dense blocks in dh_ref_layout order and the generic parameter names."""
-    if cfg.orbital != "full":
-        raise NotImplementedError("KFAC restatement covers orbital 'full' only")
     N, H, dh = cfg.nelec, cfg.num_heads, cfg.heads_dim
     D = H * dh
     M, K = int(round(cfg.flux)) + 1, cfg.determinants
@@ -101,12 +113,27 @@ def blocks(cfg: R.OracleConfig):
             generic += [p + f"LayerNorm_{j}/scale", p + f"LayerNorm_{j}/bias"]
     ob = "Orbitals_0/featured_orbitals/"
     sizes = [n for n in cfg.nspins if n > 0]
+    F = 8 if cfg.orbital == "sparse" else M  # featured orbitals per (electron, determinant)
     for blk, n in enumerate(sizes):
         for part in range(2):
             nm = ob + f"DenseGeneral_{2 * blk + part}"
-            out.append(Block(nm, nm + "/kernel", nm + "/bias", D, M * N * K, n))
+            out.append(Block(nm, nm + "/kernel", nm + "/bias", D, F * N * K, n))
+    if cfg.orbital == "sparse":
+        nm = "Orbitals_0/lll_weight"
+        out.append(Block(nm, nm + "/kernel", None, 8, M, 8 * N * N, lll=True))
+        generic.append(nm + "/bias")
     generic += ["Jastrow_0/ee_par", "Jastrow_0/ee_anti"]
     return out, generic
+
+
+def block_rows(blk: Block, x_in, dy):
+    """One walker's (inputs, output tangents) of a block as the kfac_jax rows: [rows, din]
+    and [rows, dout] (the lll_weight regrouping of the header for the complex block)."""
+    if blk.lll:
+        x = x_in.real.reshape(-1, blk.din)                       # [N, 8, N, K] row-major, groups of 8
+        g = dy.real.permute(0, 2, 3, 1).reshape(-1, blk.dout)    # [N, M, N, K] -> [N, N, K, M]
+        return x, g
+    return x_in.reshape(x_in.shape[0], -1), dy.reshape(dy.shape[0], -1)
 
 
 def batch_statistics(params, cfg: R.OracleConfig, xs, shards: int = 1):
@@ -138,15 +165,17 @@ def batch_statistics(params, cfg: R.OracleConfig, xs, shards: int = 1):
             names = list(taps)
             grads = torch.autograd.grad(FISHER_FACTOR * lp.real, [taps[n][1] for n in names] + [pr[g] for g in generic],
                                         allow_unused=True)
+            byname = {blk.name: blk for blk in bl}
             for n, gy in zip(names, grads[: len(names)]):
-                rec_x[n].append(taps[n][0])
-                rec_dy[n].append(gy)
+                xr, gr = block_rows(byname[n], taps[n][0], gy)
+                rec_x[n].append(xr)
+                rec_dy[n].append(gr)
             for g, gg in zip(generic, grads[len(names):]):
                 if gg is not None:
                     gtan[g] = gtan[g] + gg
         for blk in bl:
-            x = torch.cat([t.reshape(t.shape[0], -1) for t in rec_x[blk.name]])
-            dy = torch.cat([t.reshape(t.shape[0], -1) for t in rec_dy[blk.name]])
+            x = torch.cat(rec_x[blk.name])
+            dy = torch.cat(rec_dy[blk.name])
             rows = x.shape[0]
             if blk.bias:
                 x = torch.cat([x, torch.ones(rows, 1, dtype=DT)], 1)

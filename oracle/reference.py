@@ -218,7 +218,9 @@ def orbitals(params, cfg: OracleConfig, x, tap=_no_tap):
         # value), output moved to axis 1 (blocks.py:61-62)
         W = params["Orbitals_0/lll_weight/kernel"].to(F.real.dtype)
         b = params["Orbitals_0/lll_weight/bias"].to(F.real.dtype)
-        F = torch.einsum("najk,am->nmjk", F, W.to(F.dtype)) + b[None, :, None, None]
+        # (tap: the complex input [N, 8, N, K] and the output in this function's [N, M, N, K]
+        # layout; oracle/kfac.py regroups them as kfac_jax would)
+        F = tap("Orbitals_0/lll_weight", F, torch.einsum("najk,am->nmjk", F, W.to(F.dtype)) + b[None, :, None, None])
     env = envelope(cfg, theta, phi)  # [N, M]
     orb = (F * env[:, :, None, None]).sum(1)  # [N, N, K]
     orb = orb.permute(2, 0, 1)  # [K, N, N]

@@ -77,6 +77,26 @@ def cancellation_scales(p64, cfg, x):
             "angular_momentum_z_square": lz2_s.numpy(), "angular_momentum_z": raw["G"][:, 2].abs().numpy()}
 
 
+def fold_sparse(p64, cfg):
+    """Orbital type "sparse" (blocks.py:52-62) folded into the full layout: lll_weight (real
+    [8, M] kernel, real [M] bias) composed into each featured-orbital DenseGeneral, which is
+    linear, so the full-layout channel oracle (cancellation_scales) sees the same orbitals."""
+    import dataclasses
+
+    W = p64["Orbitals_0/lll_weight/kernel"]
+    b = p64["Orbitals_0/lll_weight/bias"]
+    out = {k: v for k, v in p64.items() if not k.startswith("Orbitals_0/lll_weight")}
+    for k, v in p64.items():
+        if k.startswith("Orbitals_0/featured_orbitals/"):
+            if k.endswith("/kernel"):  # [D, 8, N, K]
+                out[k] = torch.einsum("dajk,am->dmjk", v, W)
+            else:  # [8, N, K]; the real bias lands on the real part (DenseGeneral_even)
+                f = torch.einsum("ajk,am->mjk", v, W)
+                blk = int(k.split("DenseGeneral_")[1].split("/")[0])
+                out[k] = f + (b[:, None, None] if blk % 2 == 0 else 0.0)
+    return out, dataclasses.replace(cfg, orbital="full")
+
+
 def scaled_err(a, b, scale):
     a, b = np.asarray(a), np.asarray(b)
     return float(np.max(np.abs(a - b) / np.maximum(np.maximum(np.abs(b), 1.0), np.asarray(scale))))

@@ -87,6 +87,17 @@ def main_kfac(out, world, rank):
     stats, grad = loss_grad(params, x)
     g0 = grad.flat.clone()
     curv = loss_grad.curvature.clone()
+    extra = {}
+    if world == 1:  # the per-shard statistics two ranks would average (kfac_jax multi_device)
+        for hh, hx in enumerate((x[: B // 2], x[B // 2:])):
+            loss_grad(params, hx.contiguous())
+            extra[f"curv_h{hh}"] = loss_grad.curvature.cpu().numpy().copy()
+    # generic (NaiveDiagonal) parameters: their statistic is not additive over shards
+    gmask = torch.zeros_like(params.flat, dtype=torch.bool)
+    for k in params:
+        if "LayerNorm" in k or "Jastrow" in k or "lll_weight/bias" in k:
+            off = params[k].data_ptr() - params.flat.data_ptr()
+            gmask[off // 4: off // 4 + params[k].numel()] = True
     init, step = make_optimizer_step(cfg, model)
     state = CheckpointState(params, x, init(params), 0.1)
     p0 = params.flat.clone()
@@ -98,8 +109,8 @@ def main_kfac(out, world, rank):
     torch.cuda.synchronize()
     np.savez(f"{out}_{rank}.npz", grad=g0.cpu().numpy(), curv=curv.cpu().numpy(), p0=p0.cpu().numpy(),
              p1=snaps[0].cpu().numpy(), p2=snaps[1].cpu().numpy(), pg1=pgs[0].cpu().numpy(),
-             pg2=pgs[1].cpu().numpy(), info=state.opt_state.info.cpu().numpy(),
-             energy=complex(stats["energy"].item()))
+             pg2=pgs[1].cpu().numpy(), info=state.opt_state.info.cpu().numpy(), gmask=gmask.cpu().numpy(),
+             energy=complex(stats["energy"].item()), **extra)
 
 
 def main_nccl(out):

@@ -56,9 +56,14 @@ def _oracle_by_slot(lay, ocfg, stats, diag):
     return out, gen
 
 
-@pytest.mark.parametrize("name,B,layers", [("C1", 8, 2), ("MIX", 8, 1), ("C2", 6, 2)])
-def test_kfac_statistics_match_oracle(cuda, name, B, layers):
-    ocfg = oracle_config(name, num_layers=layers)
+@pytest.mark.parametrize("name,B,layers,orbital", [("C1", 8, 2, "full"), ("MIX", 8, 1, "full"), ("C2", 6, 2, "full"),
+                                                   ("C1", 8, 1, "sparse"), ("MIX", 6, 1, "sparse"),
+                                                   ("C2", 4, 1, "sparse")])
+def test_kfac_statistics_match_oracle(cuda, name, B, layers, orbital):
+    """Every factor slot and the generic diagonal; "sparse" orbitals (blocks.py:52-62) add the
+    8 N K-output featured blocks, the complex lll_weight block (kfac.py:127-133, 175-181;
+    oracle/kfac.py header) and its generic bias."""
+    ocfg = oracle_config(name, num_layers=layers, orbital=orbital)
     p64 = make_params(ocfg)
     system, model = build(ocfg)
     params = to_device_params(p64)
@@ -100,17 +105,17 @@ def test_kfac_vjp_with_cotangent_and_chunks(cuda):
     x = torch.tensor(make_walkers(B, ocfg.nelec, seed=33), device=cuda)
     ct = torch.tensor(np.random.default_rng(5).standard_normal((B, 2)), dtype=torch.float32, device=cuda)
     lay = _slots(model, cuda)
-    s_ref = torch.full((lay["nstats"],), float("nan"), device=cuda)
+    s_ref = torch.zeros(lay["nstats"], device=cuda)  # (the slots' alignment gaps stay 0)
     model.kfac_vjp(params, x, None, None, s_ref)
     g_ref = model.vjp(params, x, ct).flat.clone()
-    s_ct = torch.full_like(s_ref, float("nan"))
+    s_ct = torch.zeros_like(s_ref)
     g_ct = ParamTree.zeros(model.spec, cuda)
     model.kfac_vjp(params, x, ct, g_ct, s_ct)
     h = model.prepare(params, x.device)
     old = pf.VJP_WORKSPACE_BYTES
     try:
         pf.VJP_WORKSPACE_BYTES = h.lib.dh_kfac_workspace_bytes(h.h, 7)  # chunks of <= 7 walkers
-        s_ch = torch.full_like(s_ref, float("nan"))
+        s_ch = torch.zeros_like(s_ref)
         g_ch = ParamTree.zeros(model.spec, cuda)
         model.kfac_vjp(params, x, ct, g_ch, s_ch)
     finally:
@@ -125,14 +130,15 @@ def test_kfac_vjp_with_cotangent_and_chunks(cuda):
     assert (g_ch.flat - g_ref).abs().max().item() <= 2e-6 * gmax
 
 
-def test_kfac_step_matches_oracle(cuda):
-    ocfg = oracle_config("C1", num_layers=2)
+@pytest.mark.parametrize("name,B,layers,orbital", [("C1", 8, 2, "full"), ("C2", 4, 2, "full"), ("C1", 8, 1, "sparse")])
+def test_kfac_step_matches_oracle(cuda, name, B, layers, orbital):
+    ocfg = oracle_config(name, num_layers=layers, orbital=orbital)
     p64 = make_params(ocfg)
     system, model = build(ocfg)
-    x = torch.tensor(make_walkers(8, ocfg.nelec, seed=32), dtype=torch.float64)
+    x = torch.tensor(make_walkers(B, ocfg.nelec, seed=32), dtype=torch.float64)
     ref, diag = KF.batch_statistics(p64, ocfg, x)
-    ct = np.zeros((8, 2))
-    ct[:, 0] = np.random.default_rng(2).standard_normal(8)
+    ct = np.zeros((B, 2))
+    ct[:, 0] = np.random.default_rng(2).standard_normal(B)
     grads = R.logpsi_param_grad(p64, ocfg, x, ct)
     # float32 inputs shared by both sides
     ref = {k: (A.float().double(), G.float().double()) for k, (A, G) in ref.items()}

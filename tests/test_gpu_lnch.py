@@ -144,3 +144,68 @@ def test_kernel_vs_channel_oracle(cuda, N, B, mode):
           f"median {err.median():.2e} ({err32.median():.2e})")
     assert err.max() <= 2 * err32.max() + 2e-6
     assert err.median() <= 1.5 * err32.median() + 1e-8
+
+
+@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("B", [64, 5])
+def test_every_electron_slot(cuda, form, mode, B):
+    """Per electron slot of a tile (two round-3 variants of gemm_lnch gave
+    wrong values for electrons 12-15 of a tile only): kernel form 1 (16-electron tiles) and
+    form 2 (8-electron tiles, gemm_lnch2.hip, two parities per electron), full tiles (B = 64,
+    N = 6: 24 / 48 tiles) and partial ones (B = 5: 30 electrons).  Every slot's maximum error
+    against the float64 channel rules stays within 2x the torch float32 op's global maximum,
+    and no slot's median is more than 3x the overall median: a slot-dependent fault cannot
+    hide in the aggregate statistics."""
+    import ctypes as C
+
+    from deephall_amd import _lib
+    from oracle import channels as CH
+
+    lib = _lib.load()
+    N, Cc, D = 6, 17, 256
+    g = torch.Generator().manual_seed(7 * B + mode)
+    X = torch.randn(B, N, Cc, D, generator=g, dtype=torch.float64)
+    h = torch.randn(B, N, Cc, D, generator=g, dtype=torch.float64)
+    W = torch.randn(D, D, generator=g, dtype=torch.float64) / 16
+    b = torch.randn(D, generator=g, dtype=torch.float64) * 0.1
+    scale = 1 + 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    bias = 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    x = torch.stack([torch.rand(B, N, generator=g, dtype=torch.float64) * 2.8 + 0.17,
+                     torch.rand(B, N, generator=g, dtype=torch.float64) * 6.28], -1)
+    X, h, W, b, scale, bias, x = (t.float().double() for t in (X, h, W, b, scale, bias, x))
+    alpha = CH.geometry(x)["alpha"]
+
+    def ref(dt):
+        Xd, hd, Wd, bd, sd, bbd, ad = (t.to(dt) for t in (X, h, W, b, scale, bias, alpha))
+        pre = hd + (CH.linear(Xd, Wd, bd) if mode == 0 else CH.tanh_ch(CH.linear(hd, Wd, bd), ad))
+        return CH.layer_norm_ch(pre, ad, sd, bbd)
+
+    y64, y32 = ref(torch.float64), ref(torch.float32).double()
+    dev = lambda t: t.float().contiguous().to(cuda)  # noqa: E731
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    hg, Xg = dev(h.reshape(-1, D)), dev(X.reshape(-1, D))
+    st, ct, sp, cp = (f(x[..., i]) for i, f in ((0, torch.sin), (0, torch.cos), (1, torch.sin), (1, torch.cos)))
+    geo = dev(torch.stack([st, ct, sp, cp], -1).reshape(-1, 4))
+    ldp = lib.dh_debug_x6_plane_rows(D)
+    Wp = torch.empty(3 * ldp * D, dtype=torch.int16, device=cuda)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.dh_debug_split_planes(p(dev(W.t())), D, D, D, p(Wp), s) == 0
+    old = lib.dh_debug_set_lnch_form(form)
+    try:
+        assert lib.dh_debug_gemm_lnch(N, mode, p(Xg), p(Wp), ldp, p(dev(b)), p(dev(torch.cat([scale, bias]))), p(geo),
+                                      p(hg), B * N, s) == 0
+        torch.cuda.synchronize()
+    finally:
+        lib.dh_debug_set_lnch_form(old)
+    err = (hg.double().cpu().reshape(B * N, Cc, D) - y64.reshape(B * N, Cc, D)).abs()
+    lim = 2 * (y32 - y64).abs().max().item() + 2e-6
+    ept = 16 if form == 1 else 8
+    med_all = err.median().item()
+    for slot in range(ept):
+        e = err[slot::ept]
+        if e.numel() == 0:
+            continue
+        assert torch.isfinite(e).all(), slot
+        assert e.max().item() <= lim, (slot, e.max().item(), lim)
+        assert e.median().item() <= 3 * med_all + 1e-8, (slot, e.median().item(), med_all)

@@ -101,3 +101,61 @@ def test_damped_inverse_and_step():
     name = next(iter(stats))
     assert torch.allclose(st2.raw_A[name] / st2.weight, stats[name][0])
     assert np.isclose(st2.weight, 1.95)
+
+
+def test_sparse_orbital_blocks():
+    """"sparse" orbitals (blocks.py:52-62): the featured DenseGeneral blocks (8 N K outputs)
+    and the complex lll_weight block (kfac.py:127-133, 175-181).  The taps see the layers the
+    autograd gradient sees: featured blocks as in test_taps_reproduce_parameter_gradient; for
+    lll_weight, sum over (walker, i, j, k) of Re x^T Re dy + Im x^T Im dy (the natural
+    grouping: the 8-axis is the input) equals sqrt(2)^0 x the autograd gradient of the real
+    kernel.  Its KFAC statistics use kfac_jax's literal regrouping (8 x 8 and M x M factors,
+    scale 8 N^2); the lll bias is generic."""
+    cfg = oracle_config("C1", orbital="sparse", num_layers=1)
+    p = make_params(cfg)
+    B = 3
+    xs = torch.tensor(make_walkers(B, cfg.nelec, seed=4), dtype=torch.float64)
+    bl, generic = KF.blocks(cfg)
+    lll = [b for b in bl if b.lll]
+    assert len(lll) == 1 and lll[0].din == 8 and lll[0].dout == int(round(cfg.flux)) + 1
+    assert lll[0].scale == 8 * cfg.nelec**2 and "Orbitals_0/lll_weight/bias" in generic
+    ct = torch.zeros(B, 2, dtype=torch.float64)
+    ct[:, 0] = 1.0
+    grad = R.logpsi_param_grad(p, cfg, xs, ct)
+    sums = {}
+    for b in range(B):
+        taps = {}
+
+        def tap(name, x_in, y):
+            eps = torch.zeros_like(y, requires_grad=True)
+            taps[name] = (x_in.detach(), eps)
+            return y + eps
+
+        lp = R.logpsi({k: v.clone() for k, v in p.items()}, cfg, xs[b], tap)
+        gs = torch.autograd.grad(lp.real, [taps[n][1] for n in taps])
+        for n, gy in zip(taps, gs):
+            x = taps[n][0]
+            if n.endswith("lll_weight"):
+                xn = x.permute(0, 2, 3, 1).reshape(-1, 8)
+                gn = gy.permute(0, 2, 3, 1).reshape(-1, gy.shape[1])
+                s = xn.real.T @ gn.real + xn.imag.T @ gn.imag
+            else:
+                xx = torch.cat([x.reshape(x.shape[0], -1), torch.ones(x.shape[0], 1, dtype=x.dtype)], 1)
+                s = xx.T @ gy.reshape(gy.shape[0], -1)
+            sums[n] = sums.get(n, 0.0) + s
+    assert set(sums) == {blk.name for blk in bl}
+    for blk in bl:
+        gk = grad[blk.kernel].reshape(blk.din, blk.dout)
+        assert torch.allclose(sums[blk.name][: blk.din], gk, atol=1e-10 * max(1.0, gk.abs().max().item())), blk.name
+        if blk.bias:
+            assert torch.allclose(sums[blk.name][blk.din], grad[blk.bias].reshape(-1), atol=1e-10)
+    stats, diag = KF.batch_statistics(p, cfg, xs)
+    A, G = stats["Orbitals_0/lll_weight"]
+    assert A.shape == (8, 8) and G.shape == (lll[0].dout, lll[0].dout)
+    for F in (A, G):
+        assert torch.allclose(F, F.T) and torch.linalg.eigvalsh(F).min() > -1e-12 * F.abs().max().item()
+    assert diag["Orbitals_0/lll_weight/bias"].shape == (lll[0].dout,)
+    # one step through the restated update: every parameter moves, finitely
+    state = KF.KfacState()
+    new, state, info = KF.kfac_step(p, cfg, grad, state, stats, diag)
+    assert all(torch.isfinite(new[k]).all() for k in new) and 0 < info["coef"] <= 1.0
