@@ -57,12 +57,17 @@ def build(verbose: bool = False, force: bool = False) -> Path:
     if failed:
         msg = "\n".join(f"--- {s}\n{o}" for s, o in failed)
         raise RuntimeError(f"HIP build failed:\n{msg}")
-    relink = force or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs)
+    # the link manifest: a source added or removed relinks even when every object is older
+    manifest = objdir / "link.manifest"
+    names = "\n".join(o.name for o in objs)
+    relink = (force or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs)
+              or not manifest.exists() or manifest.read_text() != names)
     if relink:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+        manifest.write_text(names)
     return LIB
 
 

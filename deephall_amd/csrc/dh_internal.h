@@ -119,12 +119,7 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 // in place over h [ne * C][256]; X [ne * C][256] (mode 1: X = h); split-bf16 arithmetic.
 // DH_LNCH=0 selects the GEMM + layernorm_ch pair instead.
 bool gemm_lnch_supported(int N, int D);
-int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel, 2 gemm_lnch2_kernel; returns the previous form
-// gemm_lnch2.hip: the same operation on 16 / S-electron tiles (S channel classes), two
-// workgroups per CU, N <= 12 and 16, 20, 24
-bool gemm_lnch2_supported(int N);
-void launch_gemm_lnch2(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                       const float* geo, float* h, int ne, int mode, hipStream_t s);
+int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel; returns the previous form
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s);
 bool chain_x6_enabled();

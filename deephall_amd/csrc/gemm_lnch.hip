@@ -737,35 +737,29 @@ extern "C" int dh_debug_lnch_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-// DH_LNCH: 0 = off (GEMM + layernorm_ch), 1 = gemm_lnch_kernel (16-electron tiles, one per CU),
-// 2 = gemm_lnch2_kernel (8-electron tiles, two per CU: gemm_lnch2.hip)
+// DH_LNCH: 0 = off (GEMM + layernorm_ch), 1 = gemm_lnch_kernel (16-electron tiles, one per CU)
 static int g_lnch_form = -1;  // -1: not read yet (dh_debug_set_lnch_form overrides it)
 static int lnch_form() {
   if (g_lnch_form < 0) {
     const char* v = getenv("DH_LNCH");
-    g_lnch_form = (v && v[0] == '0') ? 0 : (v && v[0] == '2') ? 2 : 1;
+    g_lnch_form = (v && v[0] == '0') ? 0 : 1;
   }
   return g_lnch_form;
 }
 
 int set_lnch_form(int f) {
   const int old = lnch_form();
-  if (f >= 0 && f <= 2) g_lnch_form = f;
+  if (f >= 0 && f <= 1) g_lnch_form = f;
   return old;
 }
 
 bool gemm_lnch_supported(int N, int D) {
   if (D != LN_D || N < 1) return false;
-  const int f = lnch_form();
-  return f == 1 ? N <= 6 : f == 2 ? gemm_lnch2_supported(N) : false;
+  return lnch_form() == 1 && N <= 6;
 }
 
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s) {
-  if (lnch_form() == 2) {
-    launch_gemm_lnch2(N, X, Wp, ldp, bias, ln, geo, h, ne, mode, s);
-    return;
-  }
   switch (N) {
     case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
     case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
