@@ -119,10 +119,11 @@ def logpsi_f32_errors(p64, cfg, x):
 
 FLOOR_X = 1.5        # median: at most 1.5x the float32 run's
 FLOOR_X_P90 = 2.0    # 90th percentile (the 3rd-4th worst of 32 walkers: conditioning-dominated)
-FLOOR_X_MAX = 4.0    # the single worst walker (an ill-conditioned orbital matrix dominates it);
-# measured on the MI355X (tools/r03_floor_survey.sh, profiles/r03_floor_survey.txt): at most
-# 2.97x over every gate the ratio decides, except the near-pole fixtures
-FLOOR_X_MAX_POLE = 6.0  # theta within 0.15 rad of a pole: 1/sin(theta) amplifies both runs (5.2x measured)
+FLOOR_X_MAX = 4.0    # the single worst walker (an ill-conditioned orbital matrix dominates it),
+# near-pole fixtures included since round 4's cos-theta gauge (the 6x pole allowance of round 3
+# is gone).  Measured ratios on the MI355X, round 4 (tools/r04_floor_survey.sh, default mode,
+# profiles/r04_floor_survey.txt; worst gate first): median 1.17x (C5 log psi), p90 1.42x
+# (C2_sparse L^2), max 2.44x (C2_pole Lz^2; C5 log psi 1.06x) — the worst gate at 0.78 of its limit
 FLOOR_SLACK = 2e-7   # observables the float32 run happens to get (nearly) exact
 
 

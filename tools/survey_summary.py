@@ -11,21 +11,20 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
-from helpers import FLOOR_X, FLOOR_X_MAX, FLOOR_X_MAX_POLE, FLOOR_X_P90  # noqa: E402
+from helpers import FLOOR_X, FLOOR_X_MAX, FLOOR_X_P90  # noqa: E402
 
 
 def main(path):
     rows = [json.loads(line) for line in open(path)]
     gates = [r for r in rows if r.get("label")]
     print(f"# {path}: {len(gates)} gate evaluations (limits: median {FLOOR_X}x, p90 {FLOOR_X_P90}x, "
-          f"max {FLOOR_X_MAX}x / {FLOOR_X_MAX_POLE}x near the poles of the float32 run's error)")
+          f"max {FLOOR_X_MAX}x of the float32 run's error, every fixture)")
     print(f"# 'use' = the largest ratio / limit of the three; 1.0 = at the gate; 'abs' = passed on the "
           f"absolute floor (every error <= floor_abs)")
     print(f"{'gate':34s} {'med':>6s} {'p90':>6s} {'max':>6s} {'use':>6s} {'emax':>9s} {'fmax':>9s}")
     out = []
     for r in gates:
-        mx = FLOOR_X_MAX_POLE if "pole" in r["label"] else FLOOR_X_MAX
-        use = max(r["med"] / FLOOR_X, r["p90"] / FLOOR_X_P90, r["max"] / mx)
+        use = max(r["med"] / FLOOR_X, r["p90"] / FLOOR_X_P90, r["max"] / FLOOR_X_MAX)
         absok = r["emax"] <= r["floor_abs"]
         out.append((0.0 if absok else use, r, absok))
     for use, r, absok in sorted(out, key=lambda t: -t[0]):
