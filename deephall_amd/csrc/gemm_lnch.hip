@@ -70,6 +70,9 @@
 #ifndef LNCH_PERMLANE  // round-3 variant kept for the electron-slot study: the
 #define LNCH_PERMLANE 0  // four lane rows' partials summed by permlane32/16 swaps, not in LDS
 #endif
+#ifndef LNCH_LNP  // A/B knob: the LayerNorm scale / shift loaded before the output stores (1) or between them (0)
+#define LNCH_LNP 1
+#endif
 #ifndef LNCH_STAMP
 #define LNCH_STAMP 0
 #endif
@@ -657,10 +660,18 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
   for (int k = 0; k < 3; ++k) cs[k] = 3.f * au[k] * au[k] - s2 * mt[C + T + k];
   const float aL = s2 * mt[1 + T];
+  // the LayerNorm scale / shift of both column blocks before the first store: a load between
+  // two stores waits for every earlier store (vmcnt counts in order)
+  float4 lng[CB], lnb[CB];
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
-    const float4 gv = *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
-    const float4 bb = *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb);
+    lng[cb] = LNCH_LNP ? *reinterpret_cast<const float4*>(ln + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    lnb[cb] = LNCH_LNP ? *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const float4 gv = LNCH_LNP ? lng[cb] : *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
+    const float4 bb = LNCH_LNP ? lnb[cb] : *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb);
     const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bq[4] = {bb.x, bb.y, bb.z, bb.w};
     float gs[4], z0[4];
 #pragma unroll

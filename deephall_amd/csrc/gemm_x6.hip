@@ -32,7 +32,37 @@
 #include "device_common.h"
 #include "ln_ch_wave.h"
 
+#ifndef X6M_BIAS1  // A/B knob: gemm_x6m's epilogue bias loads ahead of its stores (1) or between them (0)
+#define X6M_BIAS1 1
+#endif
+#ifndef CHAIN_P3B  // A/B knob: P3 bias loads hoisted ahead of the stores (1) or between them (0)
+#define CHAIN_P3B 1
+#endif
+#ifndef CHAIN_TANH_EXP  // A/B knob: the chain kernel's tanh as 1 - 2 / (exp(2x) + 1) (2 transcendentals + 3 VALU)
+#define CHAIN_TANH_EXP 0
+#endif
+#ifndef CHAIN_STAMP  // diagnostic builds only (tools/chain_stamp.py): per-tile phase stamps of chain_x6s
+#define CHAIN_STAMP 0
+#endif
+
 namespace dh {
+
+#if CHAIN_STAMP
+// [2][CHAIN_STAMP_WG][CHAIN_NSTAMP]: slot 1 = layer 1 with its attention (NA > 0), slot 0 = the rest
+constexpr int CHAIN_STAMP_WG = 512, CHAIN_NSTAMP = 16;
+__device__ unsigned long long g_chain_stamp[2 * CHAIN_STAMP_WG * CHAIN_NSTAMP];
+#define CHAIN_T(i)                                                                                  \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < CHAIN_STAMP_WG)                                            \
+      g_chain_stamp[((NA > 0) * CHAIN_STAMP_WG + blockIdx.x) * CHAIN_NSTAMP + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+extern "C" int dh_debug_chain_stamps(unsigned long long* out, int n) {
+  n = n < 2 * CHAIN_STAMP_WG * CHAIN_NSTAMP ? n : 2 * CHAIN_STAMP_WG * CHAIN_NSTAMP;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamp), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#else
+#define CHAIN_T(i)
+#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1773,11 +1803,23 @@ __global__ __launch_bounds__(512, 1) void gemm_x6m_kernel(const float* __restric
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) bfl[rb] = (bias && (rw0 + rb * 16 + l16) % C == 0) ? 1.f : 0.f;
     if (full) {
-      // (no drain: the compiler's waits on the residual loads also cover the older DMA)
+      // (no drain: the compiler's waits on the bias / residual loads also cover the older DMA).
+      // The bias values of every column block are loaded before the first store (X6M_BIAS1):
+      // a load between two stores would wait for every earlier store (vmcnt counts in order)
+#if X6M_BIAS1
+      float4 bvs[TNC];
+#pragma unroll
+      for (int cb = 0; cb < TNC; ++cb)
+        bvs[cb] = bias ? *reinterpret_cast<const float4*>(bias + cw0 + cb * 16 + 4 * kg) : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
 #pragma unroll
       for (int cb = 0; cb < TNC; ++cb) {
         const int n = cw0 + cb * 16 + 4 * kg;
+#if X6M_BIAS1
+        const float4 bv = bvs[cb];
+#else
         const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
         float4 rv[4];
         if (HAS_R) {
 #pragma unroll
@@ -2199,6 +2241,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
   }
   const int row0 = bid * CH_BM, rows = a.rows;
+  CHAIN_T(0);
   // plane p, tile row r, column c (bf16 units)
   auto pl = [&](int p, int r, int c) __attribute__((always_inline)) {
     return smem + (size_t)p * CS_PLANE + (size_t)r * (LSP * 2) + c * 2;
@@ -2397,7 +2440,9 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     __syncthreads();
   }
   // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
+  CHAIN_T(1);
   gemm();
+  CHAIN_T(2);
   prefetch(a.Wp2, a.ldp2, 0);
   {
     float4 w0[4][4];  // feature residual: W0 rows at this lane's columns
@@ -2437,7 +2482,9 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       }
     }
   }
+  CHAIN_T(3);
   layernorm(a.ln1);  // its barriers: every wave is past its GEMM reads of the planes
+  CHAIN_T(4);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2445,7 +2492,9 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       put4(32 * rb + l32, colof(g), make_float4(x[rb][4 * g], x[rb][4 * g + 1], x[rb][4 * g + 2], x[rb][4 * g + 3]));
   __syncthreads();
   // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
+  CHAIN_T(5);
   gemm();
+  CHAIN_T(6);
   if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
@@ -2453,12 +2502,19 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     for (int g = 0; g < 4; ++g) {
       const float4 bv = *reinterpret_cast<const float4*>(a.b2 + colof(g));
       const float4 h1 = get4(32 * rb + l32, colof(g));
-      x[rb][4 * g] = h1.x + tanh_rat(acc[rb][4 * g] + bv.x);
-      x[rb][4 * g + 1] = h1.y + tanh_rat(acc[rb][4 * g + 1] + bv.y);
-      x[rb][4 * g + 2] = h1.z + tanh_rat(acc[rb][4 * g + 2] + bv.z);
-      x[rb][4 * g + 3] = h1.w + tanh_rat(acc[rb][4 * g + 3] + bv.w);
+#if CHAIN_TANH_EXP
+      auto th = [](float z) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * z) + 1.f); };
+#else
+      auto th = [](float z) { return tanh_rat(z); };
+#endif
+      x[rb][4 * g] = h1.x + th(acc[rb][4 * g] + bv.x);
+      x[rb][4 * g + 1] = h1.y + th(acc[rb][4 * g + 1] + bv.y);
+      x[rb][4 * g + 2] = h1.z + th(acc[rb][4 * g + 2] + bv.z);
+      x[rb][4 * g + 3] = h1.w + th(acc[rb][4 * g + 3] + bv.w);
     }
+  CHAIN_T(7);
   layernorm(a.ln2);
+  CHAIN_T(8);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int r = row0 + 32 * rb + l32;
@@ -2471,10 +2527,20 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
   if (!a.Wp3) return;
   __syncthreads();
+  CHAIN_T(9);
   // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
   for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
     if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
     gemm();
+    if (col0 < 3 * CH_BN) CHAIN_T(10 + 2 * (col0 / CH_BN));
+    // this lane's 16 bias values first (one wait), THEN the prefetch and the stores: a bias load
+    // between two stores waits for every earlier store (vmcnt counts in order)
+    float4 b3v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = col0 + colof(g);
+      b3v[g] = CHAIN_P3B && c + 3 < a.n3 ? *reinterpret_cast<const float4*>(a.b3 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
@@ -2485,7 +2551,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       for (int g = 0; g < 4; ++g) {
         const int c = col0 + colof(g);
         if (c + 3 < a.n3) {
-          const float4 bv = *reinterpret_cast<const float4*>(a.b3 + c);
+          const float4 bv = CHAIN_P3B ? b3v[g] : *reinterpret_cast<const float4*>(a.b3 + c);
           *reinterpret_cast<float4*>(yr + c) = make_float4(acc[rb][4 * g] + bv.x, acc[rb][4 * g + 1] + bv.y,
                                                            acc[rb][4 * g + 2] + bv.z, acc[rb][4 * g + 3] + bv.w);
         } else {
@@ -2495,6 +2561,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         }
       }
     }
+    if (col0 < 3 * CH_BN) CHAIN_T(11 + 2 * (col0 / CH_BN));
   }
 }
 
