@@ -35,6 +35,12 @@
 #ifndef X6M_BIAS1  // A/B knob: gemm_x6m's epilogue bias loads ahead of its stores (1) or between them (0)
 #define X6M_BIAS1 1
 #endif
+#ifndef CHAIN_ANT  // A/B knob: walkers per attention call in the layer-1 chain prologue (2 or 4)
+#define CHAIN_ANT 2
+#endif
+#ifndef CHAIN_APF  // A/B knob: layer 1's first weight fragments requested before (0) or after (1) the attention
+#define CHAIN_APF 0
+#endif
 #ifndef CHAIN_P3B  // A/B knob: P3 bias loads hoisted ahead of the stores (1) or between them (0)
 #define CHAIN_P3B 1
 #endif
@@ -2381,27 +2387,28 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   // ---- P1 prologue: o rows -> planes (each element split once)
   if constexpr (NA > 0) {
     static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_K == 256, "walker-aligned tiles, 4 heads x 2 wave groups");
-    constexpr int WPW = 48 / NA, PER = 2 * attn_val_floats<NA>();  // walkers per wave, staging floats
-    static_assert(WPW % 2 == 0, "walker pairs");
-    prefetch(a.Wp1, a.ldp1, 0);
+    constexpr int WPW = 48 / NA;  // walkers per wave
+    // walkers per attn_val_core call (their LDS round trips overlap): CHAIN_ANT where it divides
+    constexpr int ANT = (CHAIN_ANT == 4 && WPW % 4 == 0) ? 4 : 2, PER = ANT * attn_val_floats<NA>();
+    static_assert(WPW % 2 == 0 && CS_NW * PER * 4 <= 3 * CS_PLANE, "walker pairs, staging in the planes");
+    if (!CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0);
     float* qs = reinterpret_cast<float*>(smem) + wid * PER;
     const int hd = wid & 3, wl0 = (wid >> 2) * WPW;  // head; first tile walker of this wave
     FeatW fw;
     fw.load(a.feat.W0qkv, a.feat.bqkv, CH_K, hd * 64 + lane);
     float ov[WPW][NA];
-    // two walkers per attn_val_core call (their LDS round trips overlap); the wave-uniform
-    // guards also keep the scheduler from hoisting later walkers' loads (spills)
+    // the wave-uniform guards also keep the scheduler from hoisting later walkers' loads (spills)
 #pragma unroll
-    for (int t = 0; t < WPW; t += 2) {
+    for (int t = 0; t < WPW; t += ANT) {
       const int b = row0 / NA + wl0 + t;
-      if ((b + 2) * NA <= rows) {
-        float pq[2][NA], pk[2][NA], pv[2][NA];
-        feat_qkv<NA>(fw, a.feat.geo, b, a.feat.n_up, pq[0], pk[0], pv[0]);
-        feat_qkv<NA>(fw, a.feat.geo, b + 1, a.feat.n_up, pq[1], pk[1], pv[1]);
-        attn_val_core<NA, 2>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[2][NA]>(ov[t]));
-      } else {  // the batch ends inside this pair (last tile)
+      if ((b + ANT) * NA <= rows) {
+        float pq[ANT][NA], pk[ANT][NA], pv[ANT][NA];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < ANT; ++u) feat_qkv<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pq[u], pk[u], pv[u]);
+        attn_val_core<NA, ANT>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
+      } else {  // the batch ends inside this group (last tile)
+#pragma unroll
+        for (int u = 0; u < ANT; ++u) {
           if ((b + u + 1) * NA <= rows) {
             float pq[1][NA], pk[1][NA], pv[1][NA];
             feat_qkv<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pq[0], pk[0], pv[0]);
@@ -2413,6 +2420,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         }
       }
     }
+    if (CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0);
     __syncthreads();  // the staging areas lie in the planes
 #pragma unroll
     for (int t = 0; t < WPW; ++t)
