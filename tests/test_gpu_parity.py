@@ -354,6 +354,30 @@ def test_walker_groups_on_parallel_streams_are_bit_identical(cuda):
                 assert torch.equal(a, b), groups
 
 
+@pytest.mark.parametrize("name,B", [("C2", 4096), ("C4", 1024)])
+def test_vmc_iteration_bitwise_repeatable(cuda, name, B):
+    """One VMC iteration (4 MCMC moves + the local energy) at the bench's full-chip batch, run
+    twice from the same walkers and key: walkers, E_L, observables and accept counts equal bit
+    for bit.  A race, an early LDS read or an interleaving-dependent corruption (DESIGN 7.1,
+    the two-tiles-per-CU fused tail) shows here while every small-batch comparison passes."""
+    from deephall_amd.random import PRNGKey
+    from deephall_amd.train import make_vmc_iteration
+
+    ocfg = oracle_config(name)
+    system, model = build(ocfg)
+    params = model.init(PRNGKey(7), device=cuda)
+    x0 = init_guess(Key(13), B, ocfg.nelec, cuda, network=model)
+    it = make_vmc_iteration(model, B, 4, 1)
+    runs = []
+    for _ in range(2):
+        x, e, o, n = it(params, x0.clone(), Key(21), 0.2)
+        torch.cuda.synchronize()
+        runs.append((x.cpu(), e.cpu(), o.cpu(), n.cpu()))
+    assert torch.isfinite(runs[0][1]).all()
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def test_c3_global_batch_single_process(cuda):
     """BASELINE.json configs[2]'s global batch (32768 walkers, N=6, 2Q=15) through one
     process: MCMC, local energy (chunked by the workspace), statistics; rows are
