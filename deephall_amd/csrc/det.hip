@@ -336,13 +336,20 @@ __host__ __device__ constexpr int env_ring(int MG) { return (63 / (2 * MG) + 1) 
 // WU (short rows, C4): one WAVE per (walker, electron) instead of one workgroup: no
 // cross-wave partials, no block barriers, 4 units per workgroup (the leaves of a unit are
 // computed by its own 64 lanes).
-template <int MG, bool WU = false>
+// SEG > 0 (four waves per electron only): each wave owns a CONTIGUOUS block of MW = ceil(M / 4)
+// harmonics, so a channel row's share of a wave is two contiguous segments (re, im: MW N K
+// floats each) that come into the ring by SEG global_load_lds_dwordx4 pieces per segment (1 KiB
+// each, lanes past the segment masked) instead of 2 MG one-dword pieces: a third of the DMA
+// issue slots (an LDS-DMA piece costs ~60-180 cycles to issue, MI355X_MICROARCH.md).  Lane (j, g)
+// takes the wave's harmonics g + G u.  The launcher picks it when every piece keeps a lane.
+template <int MG, bool WU = false, int SEG = 0>
 __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restrict__ Fp, int ldF,
                                                            const float* __restrict__ x,
                                                            const float* __restrict__ geo_g,
                                                            const float* __restrict__ norm, float* __restrict__ PhiC,
                                                            int nw, int N, int n_up, int M, int K, float Q) {
-  constexpr int Q2 = 2 * MG, RING = env_ring(MG);  // load instructions per row, rows per ring
+  static_assert(SEG == 0 || !WU, "segment DMA: four waves per electron");
+  constexpr int Q2 = SEG ? 2 * SEG : 2 * MG, RING = SEG ? 4 : env_ring(MG);  // load instructions per row, rows per ring
   static_assert((RING - 1) * Q2 <= 63, "vmcnt range");
   extern __shared__ float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -355,9 +362,11 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   cf* wt = reinterpret_cast<cf*>(sm + (size_t)wv * wsz);  // [E0, DTH, DPH, LB, W0..2, SF0..2][M]
   cf* part = wt + 10 * M;                                 // [4 waves][C][N] partial sums (not WU)
   float* al = reinterpret_cast<float*>(WU ? part : part + 4 * C * N);  // [3][T]
-  float* ring = al + ((3 * T + 3) & ~3);                  // [RING][Q2][64] per wave
+  float* ring = al + ((3 * T + 3) & ~3);                  // [RING][Q2][64] per wave (SEG: [RING][2 segf])
   const int G = 64 / N, j = lane % N, g = lane / N, S = WU ? G : 4 * G;
-  const int gg = WU ? g : G * wv + g;
+  const int MW = (M + 3) / 4;                         // SEG: harmonics per wave
+  const int gg = SEG ? MW * wv + g : (WU ? g : G * wv + g);
+  const int mend = SEG ? min(MW * (wv + 1), M) : M;    // SEG: this wave's harmonics end
   const bool act = g < G;
   const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
   const int NK = N * K, MNK = M * NK;
@@ -369,12 +378,36 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   auto gsumc = [&](cf v) __attribute__((always_inline)) { return cf{gsum(v.re), gsum(v.im)}; };
   const float* rowbase = Fp + ((size_t)(b * N + i) * C) * ldF + (size_t)blk * 2 * MNK + (size_t)j * K;
   // lane's harmonic u (< MG) is m = gg + S u, valid when m < M (and g < G)
-  auto mw = [&](int u) __attribute__((always_inline)) { return min(gg + S * u, M - 1); };
-  auto okm = [&](int u) __attribute__((always_inline)) { return act && gg + S * u < M; };
-  float* wring = WU ? ring : ring + (size_t)wv * RING * Q2 * 64;
+  const int SS = SEG ? G : S;  // harmonic stride of a lane
+  auto mw = [&](int u) __attribute__((always_inline)) { return min(gg + SS * u, M - 1); };
+  auto okm = [&](int u) __attribute__((always_inline)) { return act && gg + SS * u < mend; };
+  const int segf = MW * N * K;  // SEG: floats of one segment
+  float* wring = WU ? ring : ring + (size_t)wv * RING * (SEG ? 2 * segf : Q2 * 64);
   const uint32_t ring0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)wring);
   // DMA row c of det kd into ring slot c % RING
+  // SEG: the wave's segments of row c (re at + 0, im at + MNK floats), lane-linear in the slot
+  const float* segbase = Fp + ((size_t)(b * N + i) * C) * ldF + (size_t)blk * 2 * MNK + (size_t)MW * wv * NK;
+  const int segb = (mend - MW * wv) * NK * 4;  // bytes this wave really reads per segment
   auto issue = [&](int c, int kd) __attribute__((always_inline)) {
+    if constexpr (SEG > 0) {
+      (void)kd;  // K == 1 (launcher)
+      const int slot = c % RING;
+#pragma unroll
+      for (int q = 0; q < 2 * SEG; ++q) {
+        const int p = q / SEG, piece = q % SEG;  // part (re / im), 1-KiB piece
+        const int byte = piece * 1024 + lane * 16;
+        const char* src = reinterpret_cast<const char*>(segbase + (size_t)c * ldF + (p ? (size_t)MNK : 0)) + byte;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + (uint32_t)(slot * 2 * segf * 4 + p * segf * 4 + piece * 1024));
+        if (byte < segb) {  // lane 0 of every piece is inside the segment (launcher's check)
+          unsigned keep;
+          asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                       : "=&s"(keep)
+                       : "v"(src), "s"(dst)
+                       : "memory");
+        }
+      }
+      return;
+    }
     const float* rp = rowbase + (size_t)c * ldF + kd;
     const int slot = c % RING;
 #pragma unroll
@@ -410,6 +443,10 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   auto fval = [&](int c, int u) __attribute__((always_inline)) {
+    if constexpr (SEG > 0) {
+      const float* r = wring + (size_t)(c % RING) * 2 * segf + (size_t)(g + G * u) * NK + j;  // K == 1
+      return okm(u) ? cf{r[0], r[segf]} : cf{0.f, 0.f};
+    }
     const float* r = wring + (size_t)((c % RING) * Q2 + 2 * u) * 64 + lane;
     return okm(u) ? cf{r[0], r[64]} : cf{0.f, 0.f};
   };
@@ -533,10 +570,26 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
 }
 
 // dynamic LDS of env_contract_kernel<MG, WU>
-size_t env_contract_smem(int N, int M, int MG, bool WU) {
+size_t env_contract_smem(int N, int M, int MG, bool WU, int K = 1, bool seg = false) {
   const int T = 2 * N, C = 2 * N + 5;
   if (WU) return (size_t)4 * (20 * M + ((3 * T + 3) & ~3) + env_ring(MG) * 2 * MG * 64) * sizeof(float);
-  return (size_t)(20 * M + 8 * C * N + ((3 * T + 3) & ~3) + 4 * env_ring(MG) * 2 * MG * 64) * sizeof(float);
+  const int ringf = seg ? 4 * 2 * ((M + 3) / 4) * N * K : env_ring(MG) * 2 * MG * 64;  // per wave
+  return (size_t)(20 * M + 8 * C * N + ((3 * T + 3) & ~3) + 4 * ringf) * sizeof(float);
+}
+// segment DMA (env_contract_kernel SEG > 0) usable for this shape: K == 1, 16-B aligned
+// segments, every piece of every wave keeping its lane 0, the lane harmonics within MG;
+// returns the pieces per segment (1, 2), or 0
+int env_contract_seg(int N, int M, int K, int MG, int ldF) {
+  if (K != 1 || std::getenv("DH_ENV_SEG0")) return 0;
+  const int G = 64 / N, MW = (M + 3) / 4, NK = N * K, MNK = M * NK;
+  if ((MW + G - 1) / G > MG || (MW * NK) % 4 || MNK % 4 || ldF % 4) return 0;
+  const int seg = (MW * NK * 4 + 1023) / 1024;
+  if (seg > 2) return 0;
+  for (int wv = 0; wv < 4; ++wv) {
+    const int bytes = (std::min(MW * (wv + 1), M) - MW * wv) * NK * 4;
+    if (bytes <= (seg - 1) * 1024) return 0;  // a piece without lanes would not be issued
+  }
+  return seg;
 }
 
 // ------------------------------------------------------------------ energy kernel
@@ -1380,8 +1433,8 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
     const int G = 64 / d.N;
     const int mgw = (d.M + G - 1) / G;          // harmonics per lane, one wave per electron
     const int mg = (d.M + 4 * G - 1) / (4 * G);  // harmonics per lane, four waves per electron
-    auto env = [&](auto kern, int MG, bool WU) {
-      const size_t eb = env_contract_smem(d.N, d.M, MG, WU);
+    auto env = [&](auto kern, int MG, bool WU, bool seg = false) {
+      const size_t eb = env_contract_smem(d.N, d.M, MG, WU, d.K, seg);
       ensure_smem(kern, eb);
       const int grid = WU ? (nw * d.N + 3) / 4 : nw * d.N;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(256), eb, s, F, d.ld_orb, x, geo, norm, phic, nw, d.N, d.n_up, d.M,
@@ -1400,7 +1453,16 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
         case 2: env(env_contract_kernel<2>, 2, false); break;
         case 3: env(env_contract_kernel<3>, 3, false); break;
         case 4: env(env_contract_kernel<4>, 4, false); break;
-        case 5: env(env_contract_kernel<5>, 5, false); break;
+        case 5: {
+          const int sg = env_contract_seg(d.N, d.M, d.K, 5, d.ld_orb);
+          if (sg == 2)
+            env(env_contract_kernel<5, false, 2>, 5, false, true);
+          else if (sg == 1)
+            env(env_contract_kernel<5, false, 1>, 5, false, true);
+          else
+            env(env_contract_kernel<5>, 5, false);
+          break;
+        }
         case 6: env(env_contract_kernel<6>, 6, false); break;
         case 7:
         case 8: env(env_contract_kernel<8>, 8, false); break;
