@@ -331,6 +331,10 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
 // a per-wave LDS-DMA ring (global_load_lds_dword, RING rows deep: RING - 1 rows in flight
 // without holding registers), counted with vmcnt; every lane reads back only its own words.
 // LDS-DMA ring depth: up to 4 rows, (depth - 1) rows of 2 MG loads within vmcnt's 6 bits
+#ifndef ENV_SEG_RING  // A/B knob: rows per ring of the segment-DMA form
+#define ENV_SEG_RING 4
+#endif
+constexpr int kEnvSegRing = ENV_SEG_RING;
 __host__ __device__ constexpr int env_ring(int MG) { return (63 / (2 * MG) + 1) < 4 ? (63 / (2 * MG) + 1) : 4; }
 
 // WU (short rows, C4): one WAVE per (walker, electron) instead of one workgroup: no
@@ -349,7 +353,8 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
                                                            const float* __restrict__ norm, float* __restrict__ PhiC,
                                                            int nw, int N, int n_up, int M, int K, float Q) {
   static_assert(SEG == 0 || !WU, "segment DMA: four waves per electron");
-  constexpr int Q2 = SEG ? 2 * SEG : 2 * MG, RING = SEG ? 4 : env_ring(MG);  // load instructions per row, rows per ring
+  // SEG: 4 rows per ring (ENV_SEG_RING; 5 fits 80 KiB at C5 and measured no faster)
+  constexpr int Q2 = SEG ? 2 * SEG : 2 * MG, RING = SEG ? kEnvSegRing : env_ring(MG);  // load instructions per row, rows per ring
   static_assert((RING - 1) * Q2 <= 63, "vmcnt range");
   extern __shared__ float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -425,6 +430,12 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   // wait until row c landed (rows issued after it: min(RING - 1, C - 1 - c))
   auto wait_row = [&](int c) __attribute__((always_inline)) {
     const int ahead = min(RING - 1, C - 1 - c);
+    if constexpr (RING >= 5) {
+      if (ahead >= 4) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * Q2) : "memory");
+        return;
+      }
+    }
     if constexpr (RING >= 4) {
       if (ahead >= 3) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * Q2) : "memory");
@@ -573,7 +584,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
 size_t env_contract_smem(int N, int M, int MG, bool WU, int K = 1, bool seg = false) {
   const int T = 2 * N, C = 2 * N + 5;
   if (WU) return (size_t)4 * (20 * M + ((3 * T + 3) & ~3) + env_ring(MG) * 2 * MG * 64) * sizeof(float);
-  const int ringf = seg ? 4 * 2 * ((M + 3) / 4) * N * K : env_ring(MG) * 2 * MG * 64;  // per wave
+  const int ringf = seg ? kEnvSegRing * 2 * ((M + 3) / 4) * N * K : env_ring(MG) * 2 * MG * 64;  // per wave
   return (size_t)(20 * M + 8 * C * N + ((3 * T + 3) & ~3) + 4 * ringf) * sizeof(float);
 }
 // segment DMA (env_contract_kernel SEG > 0) usable for this shape: K == 1, 16-B aligned
@@ -589,6 +600,7 @@ int env_contract_seg(int N, int M, int K, int MG, int ldF) {
     const int bytes = (std::min(MW * (wv + 1), M) - MW * wv) * NK * 4;
     if (bytes <= (seg - 1) * 1024) return 0;  // a piece without lanes would not be issued
   }
+  if (env_contract_smem(N, M, MG, false, K, true) > 163840) return 0;
   return seg;
 }
 
