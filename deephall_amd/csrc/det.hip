@@ -331,6 +331,9 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
 // a per-wave LDS-DMA ring (global_load_lds_dword, RING rows deep: RING - 1 rows in flight
 // without holding registers), counted with vmcnt; every lane reads back only its own words.
 // LDS-DMA ring depth: up to 4 rows, (depth - 1) rows of 2 MG loads within vmcnt's 6 bits
+#ifndef ENV_REG  // A/B knob: the segment form keeps the tangent rows' envelope factors in registers
+#define ENV_REG 1
+#endif
 #ifndef ENV_SEG_RING  // A/B knob: rows per ring of the segment-DMA form
 #define ENV_SEG_RING 4
 #endif
@@ -504,6 +507,21 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
     __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
   else
     __syncthreads();
+  // SEG: the four envelope factors every tangent row needs (e0, the three flow weights W_k) at
+  // this lane's harmonics, held in registers: the row loop's LDS stores (part) would keep the
+  // compiler from hoisting them, and they are 80 % of a tangent row's LDS reads
+  constexpr bool RC = SEG > 0 && ENV_REG;
+  cf re0[RC ? MG : 1], rw0[RC ? MG : 1], rw1[RC ? MG : 1], rw2[RC ? MG : 1];
+  if constexpr (RC) {
+#pragma unroll
+    for (int u = 0; u < MG; ++u) {
+      const int m = mw(u);
+      re0[u] = wt[m];
+      rw0[u] = wt[4 * M + m];
+      rw1[u] = wt[5 * M + m];
+      rw2[u] = wt[6 * M + m];
+    }
+  }
   for (int kd = 0; kd < K; ++kd) {
     cf xd{0.f, 0.f}, xp{0.f, 0.f}, xl{0.f, 0.f}, xs0{0.f, 0.f}, xs1{0.f, 0.f}, xs2{0.f, 0.f};  // F_0 extras
     cf lb2{0.f, 0.f}, gu0{0.f, 0.f}, gu1{0.f, 0.f}, gu2{0.f, 0.f};                            // lane partials
@@ -536,10 +554,10 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
         for (int u = 0; u < MG; ++u) {
           const cf fv = fval(c, u);
           const int m = mw(u);
-          cfma(e0a, fv, wt[m]);
-          cfma(w0, fv, wt[4 * M + m]);
-          cfma(w1, fv, wt[5 * M + m]);
-          cfma(w2, fv, wt[6 * M + m]);
+          cfma(e0a, fv, RC ? re0[RC ? u : 0] : wt[m]);
+          cfma(w0, fv, RC ? rw0[RC ? u : 0] : wt[4 * M + m]);
+          cfma(w1, fv, RC ? rw1[RC ? u : 0] : wt[5 * M + m]);
+          cfma(w2, fv, RC ? rw2[RC ? u : 0] : wt[6 * M + m]);
           if (own) cfma(dd, fv, wdd[m]);
         }
         gu0 += al[t] * w0;
@@ -549,7 +567,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
         if (own) e0a += (t & 1) ? xp : xd;
       } else {
 #pragma unroll
-        for (int u = 0; u < MG; ++u) cfma(e0a, fval(c, u), wt[mw(u)]);
+        for (int u = 0; u < MG; ++u) cfma(e0a, fval(c, u), RC ? re0[RC ? u : 0] : wt[mw(u)]);
         if (c == T + 1) e0a += xl + 2.f * lb2;
         if (c >= T + 2) {
           const int k = c - T - 2;
