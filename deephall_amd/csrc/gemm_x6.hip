@@ -2205,7 +2205,12 @@ __global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
 // Same products in the same order as the other x6 kernels; the LayerNorm statistics are
 // summed in a different order (f32 rounding, not bitwise).
 constexpr int CS_NW = 8, CS_RB = CH_BM / 32, CS_PD = 4, CS_LSP = 264;  // plane row: 528 B
-constexpr size_t CS_PLANE = (size_t)CH_BM * CS_LSP * 2, CS_SMEM = 3 * CS_PLANE + 2 * CS_NW * CH_BM * 4;
+#ifndef CHAIN_PRM  // A/B knob: LN1 / LN2 scale-shift and the P2 bias staged in LDS once per tile
+#define CHAIN_PRM 1
+#endif
+// CS_PRMF: [ln1 gamma | beta][b2][ln2 gamma | beta] floats after the partials (CHAIN_PRM)
+constexpr int CS_PRMF = CHAIN_PRM ? 5 * 256 : 0;
+constexpr size_t CS_PLANE = (size_t)CH_BM * CS_LSP * 2, CS_SMEM = 3 * CS_PLANE + 2 * CS_NW * CH_BM * 4 + CS_PRMF * 4;
 static_assert(CS_SMEM <= 163840, "chain LDS");
 
 // 4 f32 -> three packed bf16 pairs per term (as split3)
@@ -2238,6 +2243,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
+  float* prm = part + 2 * CS_NW * CH_BM;                         // CHAIN_PRM: [ln1 | b2 | ln2]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, lh = lane >> 5;
@@ -2248,6 +2254,10 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
   const int row0 = bid * CH_BM, rows = a.rows;
   CHAIN_T(0);
+  if (CHAIN_PRM) {  // read before the prologue's barrier
+    for (int q = tid; q < 5 * 256; q += 512)
+      prm[q] = q < 512 ? a.ln1[q] : (q < 768 ? a.b2[q - 512] : a.ln2[q - 768]);
+  }
   // plane p, tile row r, column c (bf16 units)
   auto pl = [&](int p, int r, int c) __attribute__((always_inline)) {
     return smem + (size_t)p * CS_PLANE + (size_t)r * (LSP * 2) + c * 2;
@@ -2491,7 +2501,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     }
   }
   CHAIN_T(3);
-  layernorm(a.ln1);  // its barriers: every wave is past its GEMM reads of the planes
+  layernorm(CHAIN_PRM ? prm : a.ln1);  // its barriers: every wave is past its GEMM reads of the planes
   CHAIN_T(4);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
@@ -2508,7 +2518,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.b2 + colof(g));
+      const float4 bv = *reinterpret_cast<const float4*>((CHAIN_PRM ? prm + 512 : a.b2) + colof(g));
       const float4 h1 = get4(32 * rb + l32, colof(g));
 #if CHAIN_TANH_EXP
       auto th = [](float z) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * z) + 1.f); };
@@ -2521,7 +2531,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       x[rb][4 * g + 3] = h1.w + th(acc[rb][4 * g + 3] + bv.w);
     }
   CHAIN_T(7);
-  layernorm(a.ln2);
+  layernorm(CHAIN_PRM ? prm + 768 : a.ln2);
   CHAIN_T(8);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
