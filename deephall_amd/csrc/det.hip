@@ -266,7 +266,21 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
         const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
         const float* rp = Fp + ((size_t)b * N + i) * ldF + (size_t)blk * 2 * MNK + (size_t)j * K + k;
         cf acc{0.f, 0.f};
-        for (int p = 0; p < M; ++p) cfma(acc, cf{rp[(size_t)p * NK], rp[(size_t)MNK + (size_t)p * NK]}, E0[i * M + p]);
+        // 16 harmonics' loads in flight at once (a loop with the trip count M at run time
+        // waited for every pair before its FMA: 16 L2 round trips in a row at C2); the same
+        // products summed in the same order
+        for (int p0 = 0; p0 < M; p0 += 16) {
+          float fr[16], fi[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const size_t p = (size_t)min(p0 + q, M - 1);
+            fr[q] = rp[p * NK];
+            fi[q] = rp[(size_t)MNK + p * NK];
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            if (p0 + q < M) cfma(acc, cf{fr[q], fi[q]}, E0[i * M + p0 + q]);
+        }
         A[idx] = acc;
       }
     }
