@@ -129,6 +129,7 @@ struct dh_handle {
   float* norm = nullptr;  // sqrt(binom(2Q, Q-m)), M floats (device)
   float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
   uint16_t* wp = nullptr;  // split-bf16 weight planes for the x6 kernels (device)
+  float* mqk = nullptr;    // layer 1's per-head score forms (attn_val.h, launch_lowrank_qk)
   int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
   bool params_set = false;
@@ -364,6 +365,7 @@ void dh_destroy(dh_handle* h) {
   if (h->norm) (void)hipFree(h->norm);
   if (h->wt) (void)hipFree(h->wt);
   if (h->wp) (void)hipFree(h->wp);
+  if (h->mqk) (void)hipFree(h->mqk);
   if (h->ref) (void)hipFree(h->ref);
   if (h->wb) (void)hipFree(h->wb);
   if (h->wbt) (void)hipFree(h->wbt);
@@ -426,6 +428,11 @@ void assign_packed(dh_handle* h) {
 int derive_weights(dh_handle* h, hipStream_t st) {
   const Dims& d = h->d;
   const int D = d.D;
+  if (d.L > 0 && d.dh == 64) {  // layer 1's score forms of the feature-space attention
+    if (!h->mqk) HIP_TRY(hipMalloc(&h->mqk, (size_t)d.H * kMqkStride * sizeof(float)));
+    launch_lowrank_qk(d, h->p.W0qkv, h->p.layer[0].bqkv, h->mqk, st);
+    h->p.Mqk = h->mqk;
+  }
   if (d.D % 32 == 0) {
     // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
     // NT GEMM kernels whose LDS-DMA staging wants k contiguous in both operands.
@@ -689,7 +696,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     if (!attn_in_chain) {
       const bool f = fused && l == 0;
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
-      launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr);
+      launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr,
+                       f ? P.Mqk : nullptr);
     }
     if (chain_ch) {
       const bool last = l + 1 == d.L;
@@ -709,6 +717,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       if (attn_in_chain) {
         feat.W0qkv = P.W0qkv;
         feat.bqkv = lp.bqkv;
+        feat.Mqk = P.Mqk;
       }
       launch_chain_x6(w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
                       last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,

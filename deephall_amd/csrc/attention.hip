@@ -1059,7 +1059,8 @@ template <int N, bool FEAT>
 __global__ __launch_bounds__(256) void attention_val_kernel(const float* __restrict__ qkv,
                                                             const float* __restrict__ geo, float* __restrict__ o,
                                                             int H, int ntask, const float* __restrict__ W0qkv,
-                                                            const float* __restrict__ bqkv, int n_up) {
+                                                            const float* __restrict__ bqkv, const float* __restrict__ Mqk,
+                                                            int n_up) {
   constexpr int dh = 64, PER = attn_val_floats<N>();
   extern __shared__ float sm[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1069,10 +1070,12 @@ __global__ __launch_bounds__(256) void attention_val_kernel(const float* __restr
   const int b = task / H, h = task - (task / H) * H;
   const int D = H * dh;
   float pq[1][N], pk[1][N], pv[1][N];
-  if constexpr (FEAT) {
+  float out[1][N];
+  if constexpr (FEAT) {  // scores from the features (attn_feat_core), v formed in registers
     FeatW fw;
     fw.load(W0qkv, bqkv, D, h * dh + lane);
-    feat_qkv<N>(fw, geo, b, n_up, pq[0], pk[0], pv[0]);
+    feat_v<N>(fw, geo, b, n_up, pv[0]);
+    attn_feat_core<N, 1>(Mqk + h * kMqkStride, geo, b, n_up, pv, qs, lane, out);
   } else {
     const float* base = qkv + (size_t)b * N * (3 * D) + h * dh + lane;
 #pragma unroll
@@ -1081,27 +1084,322 @@ __global__ __launch_bounds__(256) void attention_val_kernel(const float* __restr
       pk[0][i] = base[(size_t)i * 3 * D + D];
       pv[0][i] = base[(size_t)i * 3 * D + 2 * D];
     }
+    attn_val_core<N, 1>(pq, pk, pv, qs, lane, out);
   }
-  float out[1][N];
-  attn_val_core<N, 1>(pq, pk, pv, qs, lane, out);
   float* ob = o + (size_t)b * N * D + h * dh + lane;
 #pragma unroll
   for (int i = 0; i < N; ++i) ob[(size_t)i * D] = out[0][i];
 }
 
+// ---------------------------------------------------------------------------------------
+// Layer 1's CHANNEL attention in feature space (round 5; local energy, C = 2N + 5, dh = 64).
+// Every q|k|v row of layer 1 is a feature-channel vector times the folded map: with
+// f~_c,i = (f_c,i, [c == 0]) (the 4 input features of psiformer.py:51-60 or their channel
+// seeds, input.hip; the bias only on the value channel),
+//   q_c,i = f~_c,i Wq~,  k_c,j = f~_c,j Wk~,  v_c,j = f~_c,j Wv~   (Wx~ = 5 x 64 per head),
+// so every score of the channel rules (header of this file) is a 5 x 5 form with the head's
+// Mqk = s Wq~ Wk~^T (launch_lowrank_qk): s q_a,i . k_b,j = f~_a,i^T Mqk f~_b,j, and every output
+// is a 5-vector o^_c,i (the same combinations applied to f~ instead of v) times Wv~:
+//   o_c,i = o^_c,i Wv~,   o^_0 = A0 f~0,  o^_t = A_t f~0 + A0 f~t,
+//   o^_L = A_L f~0 + A0 f~L + 2 sum_t A_t f~t,  o^_Sk = A_Sk f~0 + A0 f~Sk + 2 Au_k g_k
+// (g_k,j = sum_{t of j} alpha_kt f~t,j: the flow sums of the tangent seeds).  Tangent t moves
+// only electron e = t / 2, so S_t lives on row e and column e and sum_t A_t f~t is one term per
+// tangent.  One wave per (walker, head): the N x N algebra on lanes = pairs (LDS-staged,
+// wave barriers only), the 5-vectors on lanes = (electron, component), then lane = feature
+// column d for o_c,i[d] = o^_c,i . (Wv~[:, d]) and the store: no q|k|v row is ever formed,
+// the 64-wide dots of attention_wave_kernel<N, true> become 30-FMA forms per pair.
 template <int N>
-void launch_wave(const Dims& d, const float* qkv, const float* W0qkv, const float* bqkv, const float* geo, float* o,
-                 int nw, int C, hipStream_t s) {
+struct FeatAttnSmem {
+  static constexpr int nn = N * N, T = 2 * N;
+  static constexpr int M = 0, G = 32, F0 = G + 4 * N, FC = F0 + 5 * N, GK = FC + 5 * N, AL = GK + 15 * N,
+                       ACC = AL + 3 * T, OL = ACC + N, OH = OL + 5 * N, A0 = OH + 5 * N, T2 = A0 + nn,
+                       SUB = T2 + nn, AU = SUB + 3 * nn, QK = AU + 3 * nn, S = QK + 3 * nn, P = S + nn,
+                       RM = P + nn, TOTAL = RM + nn;
+};
+
+template <int N>
+__global__ __launch_bounds__(64) void attention_feat_kernel(const float* __restrict__ geo, float* __restrict__ o,
+                                                            int H, const float* __restrict__ W0qkv,
+                                                            const float* __restrict__ bqkv,
+                                                            const float* __restrict__ Mqk, int n_up) {
+  constexpr int dh = 64, T = 2 * N, C = 2 * N + 5, nn = N * N;
+  using L = FeatAttnSmem<N>;
+  extern __shared__ float sm[];
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H, lane = threadIdx.x;
+  const int D = H * dh;
+  auto wsync = [] { __builtin_amdgcn_wave_barrier(); };
+  float *Ms = sm + L::M, *g = sm + L::G, *f0 = sm + L::F0, *fc = sm + L::FC, *gk = sm + L::GK, *al = sm + L::AL;
+  float *accS = sm + L::ACC, *oL = sm + L::OL, *oh = sm + L::OH, *A0 = sm + L::A0, *T2 = sm + L::T2;
+  float *SuB = sm + L::SUB, *Au = sm + L::AU, *QK = sm + L::QK, *S = sm + L::S, *P = sm + L::P, *Rm = sm + L::RM;
+  // this lane's output column: Wv~[:, d] = (W0 Wv rows, bv)
+  const int col = h * dh + lane;
+  const float4 wv = make_float4(W0qkv[2 * D + col], W0qkv[3 * D + 2 * D + col], W0qkv[6 * D + 2 * D + col],
+                                W0qkv[9 * D + 2 * D + col]);
+  const float bv = bqkv[2 * D + col];
+  if (lane < 25) Ms[lane] = Mqk[h * kMqkStride + lane];
+  for (int i = lane; i < N; i += 64) {
+    const float4 gi = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    g[4 * i] = gi.x;
+    g[4 * i + 1] = gi.y;
+    g[4 * i + 2] = gi.z;
+    g[4 * i + 3] = gi.w;
+    const float4 f = feature_channel<T>(0, i, gi, (i < n_up) ? 1.f : -1.f);
+    f0[5 * i] = f.x;
+    f0[5 * i + 1] = f.y;
+    f0[5 * i + 2] = f.z;
+    f0[5 * i + 3] = f.w;
+    f0[5 * i + 4] = 1.f;
+    accS[i] = 0.f;
+  }
+  for (int q = lane; q < 5 * N; q += 64) oL[q] = 0.f;
+  for (int p = lane; p < nn; p += 64) {
+    T2[p] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) SuB[k * nn + p] = Au[k * nn + p] = 0.f;
+  }
+  wsync();
+  for (int t = lane; t < T; t += 64) {
+    const int i = t >> 1;
+    const float st = g[4 * i], ct = g[4 * i + 1], sp = g[4 * i + 2], cp = g[4 * i + 3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((t & 1) == 0)
+        a = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+      else
+        a = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+      al[k * T + t] = a;
+    }
+  }
+  for (int q = lane; q < 3 * N; q += 64) {  // g_k,i: alpha-weighted tangent seeds of electron i
+    const int k = q / N, i = q - k * N;
+    const float st = g[4 * i], ct = g[4 * i + 1], sp = g[4 * i + 2], cp = g[4 * i + 3];
+    const float ae = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+    const float ao = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+    float* d = gk + (k * N + i) * 5;
+    d[0] = -ae * st;
+    d[1] = ae * ct * cp - ao * sp;
+    d[2] = ae * ct * sp + ao * cp;
+    d[3] = 0.f;
+    d[4] = 0.f;
+  }
+  float Mr[25];
+  wsync();
+#pragma unroll
+  for (int q = 0; q < 25; ++q) Mr[q] = Ms[q];
+  // x^T Mqk y of two 5-vectors in LDS
+  auto form = [&](const float* x, const float* y) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      float u = 0.f;
+#pragma unroll
+      for (int c2 = 0; c2 < 5; ++c2) u = fmaf(Mr[5 * a + c2], y[c2], u);
+      s = fmaf(x[a], u, s);
+    }
+    return s;
+  };
+  // o_c,i[d] for every electron (lane = d) from the 5-vectors oh[i]
+  float* obase = o + (size_t)b * N * C * D + col;
+  auto expand = [&](int c) {
+    wsync();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float* u = oh + 5 * i;
+      const float v = fmaf(u[0], wv.x, fmaf(u[1], wv.y, fmaf(u[2], wv.z, fmaf(u[3], wv.w, u[4] * bv))));
+      obase[(size_t)(i * C + c) * D] = v;
+    }
+  };
+  // the current channel's seeds f~_c,i (bias component 0) into fc
+  auto seeds = [&](int c) {
+    for (int i = lane; i < N; i += 64) {
+      const float4 gi = make_float4(g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]);
+      const float4 f = feature_channel<T>(c, i, gi, (i < n_up) ? 1.f : -1.f);
+      fc[5 * i] = f.x;
+      fc[5 * i + 1] = f.y;
+      fc[5 * i + 2] = f.z;
+      fc[5 * i + 3] = f.w;
+      fc[5 * i + 4] = 0.f;
+    }
+  };
+
+  // ---- value channel: A0 = softmax(f~0 Mqk f~0^T), o^_0 = A0 f~0
+  for (int p = lane; p < nn; p += 64) {
+    const int i = p / N, j = p - (p / N) * N;
+    A0[p] = form(f0 + 5 * i, f0 + 5 * j);
+  }
+  wsync();
+  for (int i = lane; i < N; i += 64) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A0[i * N + j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A0[i * N + j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A0[i * N + j] = e[j] * inv;
+  }
+  wsync();
+  for (int q = lane; q < 5 * N; q += 64) {
+    const int i = q / 5, a = q - (q / 5) * 5;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc = fmaf(A0[i * N + j], f0[5 * j + a], acc);
+    oh[q] = acc;
+  }
+  expand(0);
+
+  // ---- tangents: S_t on row / column e = t / 2 only
+  for (int t = 0; t < T; ++t) {
+    const int c = 1 + t, e = t >> 1;
+    wsync();
+    seeds(c);  // only row e is nonzero
+    wsync();
+    const float* fe = fc + 5 * e;
+    for (int p = lane; p < nn; p += 64) {
+      const int i = p / N, j = p - (p / N) * N;
+      float s = 0.f;
+      if (i == e) s += form(fe, f0 + 5 * j);
+      if (j == e) s += form(f0 + 5 * i, fe);
+      S[p] = s;
+      if (i == e && j == e) accS[e] += 2.f * form(fe, fe);  // s q_t . k_t, twice (S_L)
+    }
+    wsync();
+    for (int p = lane; p < nn; p += 64) {
+      const int i = p / N;
+      float m1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
+      const float sb = S[p] - m1, at = A0[p] * sb;
+      T2[p] = fmaf(sb, sb, T2[p]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float a = al[k * T + t];
+        SuB[k * nn + p] = fmaf(a, sb, SuB[k * nn + p]);
+        Au[k * nn + p] = fmaf(a, at, Au[k * nn + p]);
+      }
+      Rm[p] = at;
+    }
+    wsync();
+    for (int q = lane; q < 5 * N; q += 64) {
+      const int i = q / 5, a = q - (q / 5) * 5;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], f0[5 * j + a], acc);
+      acc = fmaf(A0[i * N + e], fe[a], acc);
+      oL[q] = fmaf(2.f * Rm[i * N + e], fe[a], oL[q]);
+      oh[q] = acc;
+    }
+    expand(c);
+  }
+  // ---- flow score terms 2 s qu_k . ku_k = 2 g_k,i^T Mqk g_k,j
+  wsync();
+  for (int p = lane; p < 3 * nn; p += 64) {
+    const int k = p / nn, pp = p - k * nn, i = pp / N, j = pp - (pp / N) * N;
+    QK[p] = 2.f * form(gk + (k * N + i) * 5, gk + (k * N + j) * 5);
+  }
+  // ---- Laplace-Beltrami and flow channels (dense seeds on every electron)
+#pragma unroll 1
+  for (int c = T + 1; c < C; ++c) {
+    const int k = c - T - 2;  // flow axis (k < 0: the Laplace-Beltrami channel)
+    wsync();
+    seeds(c);
+    wsync();
+    for (int p = lane; p < nn; p += 64) {
+      const int i = p / N, j = p - (p / N) * N;
+      float s = form(fc + 5 * i, f0 + 5 * j) + form(f0 + 5 * i, fc + 5 * j);
+      if (k < 0) {
+        if (i == j) s += accS[i];
+        P[p] = T2[p];
+      } else {
+        s += QK[k * nn + p];
+        const float u = SuB[k * nn + p];
+        P[p] = u * u;
+      }
+      S[p] = s;
+    }
+    wsync();
+    for (int p = lane; p < nn; p += 64) {
+      const int i = p / N;
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
+        m2 = fmaf(A0[i * N + j], P[i * N + j], m2);
+      }
+      Rm[p] = A0[p] * ((S[p] - m1) + (P[p] - m2));
+    }
+    wsync();
+    for (int q = lane; q < 5 * N; q += 64) {
+      const int i = q / 5, a = q - (q / 5) * 5;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], f0[5 * j + a], fmaf(A0[i * N + j], fc[5 * j + a], acc));
+      if (k < 0) {
+        acc += oL[q];
+      } else {
+        float a2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) a2 = fmaf(Au[k * nn + i * N + j], gk[(k * N + j) * 5 + a], a2);
+        acc = fmaf(2.f, a2, acc);
+      }
+      oh[q] = acc;
+    }
+    expand(c);
+  }
+}
+
+// DH_ATTN_FEAT=0 keeps attention_wave_kernel<N, true> / the MFMA kernel for layer 1's channel
+// attention (A/B measurements)
+static bool attn_feat_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_ATTN_FEAT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int N>
+void launch_feat(const Dims& d, const float* geo, float* o, int nw, const float* W0qkv, const float* bqkv,
+                 const float* Mqk, hipStream_t s) {
+  const size_t smem = (size_t)FeatAttnSmem<N>::TOTAL * sizeof(float);
+  ensure_smem(attention_feat_kernel<N>, smem);
+  hipLaunchKernelGGL(attention_feat_kernel<N>, dim3(nw * d.H), dim3(64), smem, s, geo, o, d.H, W0qkv, bqkv, Mqk,
+                     d.n_up);
+}
+
+__global__ void lowrank_qk_kernel(const float* __restrict__ W0qkv, const float* __restrict__ bqkv, int D, int H,
+                                  float* __restrict__ Mqk) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= H * 25) return;
+  const int h = t / 25, a = (t % 25) / 5, c = t % 5, ld = 3 * D;
+  double s = 0.0;
+  for (int e = 0; e < 64; ++e) {
+    const int col = h * 64 + e;
+    const double q = a < 4 ? (double)W0qkv[a * ld + col] : (double)bqkv[col];
+    const double k = c < 4 ? (double)W0qkv[c * ld + D + col] : (double)bqkv[D + col];
+    s += q * k;
+  }
+  Mqk[h * kMqkStride + 5 * a + c] = (float)(0.125 * s);
+}
+
+template <int N>
+void launch_wave(const Dims& d, const float* qkv, const float* W0qkv, const float* bqkv, const float* Mqk,
+                 const float* geo, float* o, int nw, int C, hipStream_t s) {
   const int nn = N * N;
   if (C == 1) {
     const int ntask = nw * d.H;
     const size_t smem = (size_t)4 * (2 * N * 68 + nn) * sizeof(float);
     if (W0qkv)
       hipLaunchKernelGGL((attention_val_kernel<N, true>), dim3((ntask + 3) / 4), dim3(256), smem, s, qkv, geo, o,
-                         d.H, ntask, W0qkv, bqkv, d.n_up);
+                         d.H, ntask, W0qkv, bqkv, Mqk, d.n_up);
     else
       hipLaunchKernelGGL((attention_val_kernel<N, false>), dim3((ntask + 3) / 4), dim3(256), smem, s, qkv, geo, o,
-                         d.H, ntask, W0qkv, bqkv, d.n_up);
+                         d.H, ntask, W0qkv, bqkv, Mqk, d.n_up);
     return;
   }
   const size_t smem = (size_t)((N > 8 ? 4 : 6) * N * 68 + 15 * nn + 6 * N) * sizeof(float);  // VR above
@@ -1131,26 +1429,44 @@ bool attention_takes_features(const Dims& d, int C) {
   return d.dh == 64 && (d.N <= 8 || d.N == 10 || d.N == 20);
 }
 
+void launch_lowrank_qk(const Dims& d, const float* W0qkv, const float* bqkv, float* Mqk, hipStream_t s) {
+  hipLaunchKernelGGL(lowrank_qk_kernel, dim3((d.H * 25 + 127) / 128), dim3(128), 0, s, W0qkv, bqkv, d.D, d.H, Mqk);
+}
+
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
-                      const float* W0qkv, const float* bqkv) {
+                      const float* W0qkv, const float* bqkv, const float* Mqk) {
   // wave kernels (value and channel) for dh = 64, N <= 8; W0qkv != nullptr selects the
   // fused layer-1 form (q|k|v from the input features), valid only for those kernels.
+  if (C > 1 && W0qkv && Mqk && d.dh == 64 && attn_feat_enabled() && attention_takes_features(d, C)) {
+    switch (d.N) {  // layer 1, feature space (attention_feat_kernel)
+      case 1: launch_feat<1>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 2: launch_feat<2>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 3: launch_feat<3>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 4: launch_feat<4>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 5: launch_feat<5>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 6: launch_feat<6>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 7: launch_feat<7>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 8: launch_feat<8>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      case 10: launch_feat<10>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+      default: launch_feat<20>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+    }
+  }
   if (C > 1 && attention_mfma_supported(d)) {
     launch_attention_mfma(d, qkv, geo, o, nw, s, W0qkv, bqkv);
     return;
   }
   if (attention_takes_features(d, C)) {
     switch (d.N) {
-      case 1: launch_wave<1>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 2: launch_wave<2>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 3: launch_wave<3>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 4: launch_wave<4>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 5: launch_wave<5>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 6: launch_wave<6>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 7: launch_wave<7>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 8: launch_wave<8>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      case 10: launch_wave<10>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
-      default: launch_wave<20>(d, qkv, W0qkv, bqkv, geo, o, nw, C, s); return;
+      case 1: launch_wave<1>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 2: launch_wave<2>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 3: launch_wave<3>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 4: launch_wave<4>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 5: launch_wave<5>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 6: launch_wave<6>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 7: launch_wave<7>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 8: launch_wave<8>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      case 10: launch_wave<10>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
+      default: launch_wave<20>(d, qkv, W0qkv, bqkv, Mqk, geo, o, nw, C, s); return;
     }
   }
   // channel kernel v2 needs dh <= 64 (one feature column per lane) and dh % 4 == 0;

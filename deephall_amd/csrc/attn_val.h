@@ -109,4 +109,90 @@ __device__ __forceinline__ void attn_val_core(const float (&pq)[NT][N], const fl
   }
 }
 
+// Layer 1's scores straight from the input features (round 5).  With f~ = (z, x, y, spin, 1)
+// and the q / k biases as the fifth rows of the folded maps, q_i = f~_i Wq~, k_j = f~_j Wk~, so
+//   S_ij = q_i . k_j / sqrt(64) = f~_i^T Mqk f~_j,   Mqk = Wq~ Wk~^T / 8   (5 x 5 per head)
+// — 30 FMAs per score pair from the electrons' geometry instead of staging the 64-wide q, k
+// rows in LDS and forming the dots.  Mqk is formed once per parameter upload (attention.hip
+// lowrank_qk_kernel, f64 sums); attn_val_core's softmax and value sums follow unchanged.
+__device__ __forceinline__ void feat5(const float* __restrict__ geo, int row, bool up, float (&f)[5]) {
+  const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)row);  // st ct sp cp
+  f[0] = g.y;
+  f[1] = g.x * g.w;
+  f[2] = g.x * g.z;
+  f[3] = up ? 1.f : -1.f;
+  f[4] = 1.f;
+}
+template <int N>
+__host__ __device__ constexpr int attn_feat_floats() { return N * N; }
+
+// NT walkers b0 .. b0 + NT - 1 of one head (Mh: its 25 Mqk entries, row-major); pv: this lane's
+// column of v per task and electron (feat_qkv); st: NT x attn_feat_floats(N) floats of
+// wave-private LDS; out[t][i] = o of task t, electron i, column d = lane.
+template <int N, int NT>
+__device__ __forceinline__ void attn_feat_core(const float* __restrict__ Mh, const float* __restrict__ geo, int b0,
+                                               int n_up, const float (&pv)[NT][N], float* st, int lane,
+                                               float (&out)[NT][N]) {
+  constexpr int nn = N * N, PER = attn_feat_floats<N>();
+  float M[25];
+#pragma unroll
+  for (int q = 0; q < 25; ++q) M[q] = Mh[q];
+  __builtin_amdgcn_wave_barrier();  // a previous call's readers of st (LDS ops of a wave run in order)
+  for (int p = lane; p < NT * nn; p += 64) {
+    const int t = p / nn, pair = p - t * nn, i = pair / N, j = pair - (pair / N) * N;
+    float fi[5], fj[5];
+    feat5(geo, (b0 + t) * N + i, i < n_up, fi);
+    feat5(geo, (b0 + t) * N + j, j < n_up, fj);
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      float u = 0.f;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) u = fmaf(M[5 * a + c], fj[c], u);
+      s = fmaf(fi[a], u, s);
+    }
+    st[t * PER + pair] = s;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < NT * N) {  // lane = (task, row): softmax over j (as attn_val_core)
+    const int t = lane / N, r = lane - t * N;
+    float* A = st + t * PER + r * N;
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A[j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A[j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A[j] = e[j] * inv;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float* A = st + t * PER;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(A[i * N + j], pv[t][j], acc);
+      out[t][i] = acc;
+    }
+  }
+}
+
+// this lane's column of v only (feat_qkv without q and k: the scores come from Mqk)
+template <int N>
+__device__ __forceinline__ void feat_v(const FeatW& fw, const float* __restrict__ geo, int b, int n_up, float (&pv)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+    const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (i < n_up) ? 1.f : -1.f);
+    pv[i] = FeatW::dot(f, fw.wv) + fw.bv;
+  }
+}
+
 }  // namespace dh

@@ -16,6 +16,7 @@
 // Jastrow, potential and the KE / Lz / Lz^2 / L^2 assembly (DESIGN.md §3.4,
 // equivalent to hamiltonian.py:115-169).
 #include <cstdlib>
+#include <type_traits>
 
 #include "dh_internal.h"
 #include "device_common.h"
@@ -146,7 +147,7 @@ __device__ inline void find_pivot(const cf* A, int lda, int N, int p, int* piv, 
 // Accumulates log det into logdet (complex, phase unwrapped).  Uses __syncthreads.
 // tid / nt: this walker's threads (default the whole block; det_value's half-wave form
 // passes its 32 lanes and width 32 for the pivot search).
-__device__ void eliminate(cf* A, int lda, int N, int ncol, bool gj, cf* fac, int* piv, cf* logdet,
+__device__ __forceinline__ void eliminate(cf* A, int lda, int N, int ncol, bool gj, cf* fac, int* piv, cf* logdet,
                           int tid = threadIdx.x, int nt = blockDim.x, int width = 64) {
   if (tid == 0) *logdet = cf{0.f, 0.f};
   __syncthreads();
@@ -728,6 +729,215 @@ __device__ inline void block_sum4(float v[4], float* red) {
   __syncthreads();
 }
 
+// ---- combine determinants, Jastrow, potential, assembly (double precision).
+// Per-tangent terms on threads t < T, per-electron Jastrow / potential sums on threads
+// T + i, partial results in LDS; thread 0 finishes with scalar sums only (no private
+// arrays, so nothing goes to scratch memory).
+// Shared by det_energy_kernel and det_energy_wave_kernel: ell0 [K], ellt [K T], ellL [K],
+// ellS [3 K] (written by thread 0 / the lanes before the call), geometry geo (f32) / dgeo
+// (f64) / al in LDS, asmb = 2 (4 T + 3 N) floats of LDS scratch; every thread of the
+// workgroup calls it (one __syncthreads inside), threads tid < T + N do the per-tangent and
+// per-electron parts.
+__device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M, int K, float Q, float radius, float lambda,
+                                int interaction, int b, const float* __restrict__ x, const float* __restrict__ jas,
+                                const float* geo, const double* dgeo, const float* al, const cf* ell0,
+                                const cf* ellt, const cf* ellL, const cf* ellS, double* asmb,
+                                float* __restrict__ e_l, float* __restrict__ obs) {
+  const int T = 2 * N;
+  __syncthreads();  // ell* written by thread 0 in the channel loops
+  double* tgr = asmb;
+  double* tgi = tgr + T;
+  double* lbr = tgi + T;
+  double* lbi = lbr + T;
+  double* Jn = lbi + T;
+  double* Jlbn = Jn + N;
+  double* pen = Jlbn + N;
+  // determinant weights p_k = w_k / Z, w_k = exp(ell0_k - max) (every thread; K is small)
+  double lmax = -1e300;
+  for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
+  double zr = 0.0, zi = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double mag = exp((double)ell0[k].re - lmax);
+    zr += mag * cos((double)ell0[k].im);
+    zi += mag * sin((double)ell0[k].im);
+  }
+  const double zz = zr * zr + zi * zi;
+  auto pk = [&](int k, double& pr, double& pi_) {
+    const double mag = exp((double)ell0[k].re - lmax);
+    const double wr = mag * cos((double)ell0[k].im), wi = mag * sin((double)ell0[k].im);
+    pr = (wr * zr + wi * zi) / zz;
+    pi_ = (wi * zr - wr * zi) / zz;
+  };
+  const double ap = jas[0], aa = jas[1];
+  if (tid < T) {
+    const int t = tid, i = t >> 1;
+    double gr = 0.0, gi = 0.0, sr = 0.0, si = 0.0;
+    for (int k = 0; k < K; ++k) {
+      double pr, pi_;
+      pk(k, pr, pi_);
+      const double lr = ellt[k * T + t].re, li = ellt[k * T + t].im;
+      gr += pr * lr - pi_ * li;
+      gi += pr * li + pi_ * lr;
+      const double l2r = lr * lr - li * li, l2i = 2.0 * lr * li;
+      sr += pr * l2r - pi_ * l2i;
+      si += pr * l2i + pi_ * l2r;
+    }
+    lbr[t] = sr - (gr * gr - gi * gi);
+    lbi[t] = si - 2.0 * gr * gi;
+    // Jastrow gradient along the (scaled) tangent t of electron i
+    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
+    const double ri[3] = {sti * cpi, sti * spi, cti};
+    const double et[3] = {(t & 1) ? -spi : cti * cpi, (t & 1) ? cpi : cti * spi, (t & 1) ? 0.0 : -sti};
+    double jg = 0.0;
+    for (int j = 0; j < N; ++j) {
+      if (j == i) continue;
+      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
+      const double rj[3] = {stj * cpj, stj * spj, ctj};
+      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
+      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
+      const bool same = (i < n_up) == (j < n_up);
+      double f1, f2;
+      (void)jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+      jg += (-f1 / r) * (rj[0] * et[0] + rj[1] * et[1] + rj[2] * et[2]);
+    }
+    // gauge term A = i sum_i kappa_i phi_i (env_leaf) on the phi tangent
+    if (t & 1) gi += (double)env_gauge(geo[4 * i + 1], M) / sti;  // the leaves' kappa
+    tgr[t] = gr + jg;
+    tgi[t] = gi;
+  } else if (tid < T + N) {
+    const int i = tid - T;
+    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
+    const double ri[3] = {sti * cpi, sti * spi, cti};
+    double J = 0.0, Jlb = 0.0, pe = 0.0;
+    for (int j = i + 1; j < N; ++j) {
+      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
+      const double rj[3] = {stj * cpj, stj * spj, ctj};
+      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
+      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
+      const bool same = (i < n_up) == (j < n_up);
+      double f1, f2;
+      J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
+      Jlb += 2.0 * ((4.0 - r * r) * r * f2 + (4.0 - 3.0 * r * r) * f1) / (4.0 * r);
+      if (interaction == DH_INTERACTION_COULOMB)
+        pe += 1.0 / sqrt(2.0 - 2.0 * u);
+      else
+        pe += 1.0 + ((double)Q + 1.0) / (double)Q * u;
+    }
+    Jn[i] = J;
+    Jlbn[i] = Jlb;
+    pen[i] = pe;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double val_re = 0.5 * log(zz) + lmax, val_im = atan2(zi, zr);
+    double LB_re = 0.0, LB_im = 0.0;
+    for (int k = 0; k < K; ++k) {
+      double pr, pi_;
+      pk(k, pr, pi_);
+      LB_re += pr * ellL[k].re - pi_ * ellL[k].im;
+      LB_im += pr * ellL[k].im + pi_ * ellL[k].re;
+    }
+    for (int t = 0; t < T; ++t) {
+      LB_re += lbr[t];
+      LB_im += lbi[t];
+    }
+    double S_re[3], S_im[3];
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      double a_r = 0.0, a_i = 0.0, m1r = 0.0, m1i = 0.0, m2r = 0.0, m2i = 0.0;
+      for (int k = 0; k < K; ++k) {
+        double pr, pi_;
+        pk(k, pr, pi_);
+        a_r += pr * ellS[3 * k + kk].re - pi_ * ellS[3 * k + kk].im;
+        a_i += pr * ellS[3 * k + kk].im + pi_ * ellS[3 * k + kk].re;
+        double gur = 0.0, gui = 0.0;
+        for (int t = 0; t < T; ++t) {
+          gur += (double)al[kk * T + t] * ellt[k * T + t].re;
+          gui += (double)al[kk * T + t] * ellt[k * T + t].im;
+        }
+        m1r += pr * gur - pi_ * gui;
+        m1i += pr * gui + pi_ * gur;
+        const double g2r = gur * gur - gui * gui, g2i = 2.0 * gur * gui;
+        m2r += pr * g2r - pi_ * g2i;
+        m2i += pr * g2i + pi_ * g2r;
+      }
+      S_re[kk] = a_r + m2r - (m1r * m1r - m1i * m1i);
+      S_im[kk] = a_i + m2i - 2.0 * m1r * m1i;
+    }
+    double J = 0.0, Jlb = 0.0, pe = 0.0;
+    for (int i = 0; i < N; ++i) {
+      J += Jn[i];
+      Jlb += Jlbn[i];
+      pe += pen[i];
+    }
+    if (interaction == DH_INTERACTION_COULOMB) pe /= (double)radius;
+    // gauge terms: phase and the flow channels' phi acceleration (see env_flow2)
+    double gauge_phase = 0.0;
+    for (int i = 0; i < N; ++i) {
+      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
+      const double kap = (double)env_gauge(geo[4 * i + 1], M);  // the leaves' kappa
+      gauge_phase += kap * (double)x[2 * (b * N + i) + 1];
+      const double cot = ct / st;
+      const double tdot[3] = {-sp, cp, 0.0};
+      const double thp[3] = {cp * cot, sp * cot, -1.0};
+      const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
+      const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) S_im[kk] += kap * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
+    }
+    pe *= (double)lambda;
+    LB_re += Jlb;
+    double sq_re = 0.0, sq_im = 0.0, mag_re = 0.0, mag_im = 0.0;
+    for (int t = 0; t < T; ++t) {
+      sq_re += tgr[t] * tgr[t] - tgi[t] * tgi[t];
+      sq_im += 2.0 * tgr[t] * tgi[t];
+    }
+    double Mv[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < N; ++i) {
+      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
+      const double cot = ct / st;
+      mag_re += (Q * cot) * (Q * cot);
+      mag_re += -2.0 * Q * cot * tgi[2 * i + 1];  // 2 i Q cot * t_phi_scaled
+      mag_im += 2.0 * Q * cot * tgr[2 * i + 1];
+      Mv[0] += Q * cp / st;
+      Mv[1] += Q * sp / st;
+    }
+    const double r2 = (double)radius * radius;
+    const double ke_re = (-LB_re - sq_re + mag_re) / (2.0 * r2);
+    const double ke_im = (-LB_im - sq_im + mag_im) / (2.0 * r2);
+    double G_re[3], G_im[3];
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      double gr = 0.0, gi = 0.0;
+      for (int t = 0; t < T; ++t) {
+        gr += (double)al[kk * T + t] * tgr[t];
+        gi += (double)al[kk * T + t] * tgi[t];
+      }
+      G_re[kk] = gr;
+      G_im[kk] = gi;
+    }
+    double L2 = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      const double ar = G_re[kk], ai = G_im[kk] + Mv[kk];  // (G + i M)^2, real part
+      L2 -= S_re[kk] + (ar * ar - ai * ai);
+    }
+    const double lz = G_im[2];
+    const double lz2 = -(S_re[2] + G_re[2] * G_re[2] - G_im[2] * G_im[2]);
+    e_l[2 * b] = (float)(ke_re + pe);
+    e_l[2 * b + 1] = (float)ke_im;
+    float* ob = obs + 8 * (size_t)b;
+    ob[0] = (float)ke_re;
+    ob[1] = (float)ke_im;
+    ob[2] = (float)pe;
+    ob[3] = (float)lz;
+    ob[4] = (float)lz2;
+    ob[5] = (float)L2;
+    ob[6] = (float)(val_re + J);
+    ob[7] = (float)remainder(val_im + gauge_phase, 2.0 * M_PI);
+  }
+}
+
 // PF > 0: orbital rows staged through LDS, PF floats per thread in flight.
 // PC: the channel matrices come precontracted from env_contract_kernel (PhiC), F unused.
 // NT: threads per walker, 256 (four waves; the default) or 64 (one wave, DH_DET_WAVE=1:
@@ -1014,202 +1224,332 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
     __syncthreads();
   }
 
-  // ---- combine determinants, Jastrow, potential, assembly (double precision).
-  // Per-tangent terms on threads t < T, per-electron Jastrow / potential sums on threads
-  // T + i, partial results in LDS; thread 0 finishes with scalar sums only (no private
-  // arrays, so nothing goes to scratch memory).
-  __syncthreads();  // ell* written by thread 0 in the channel loops
-  double* tgr = reinterpret_cast<double*>(sm + L.asmb);
-  double* tgi = tgr + T;
-  double* lbr = tgi + T;
-  double* lbi = lbr + T;
-  double* Jn = lbi + T;
-  double* Jlbn = Jn + N;
-  double* pen = Jlbn + N;
-  // determinant weights p_k = w_k / Z, w_k = exp(ell0_k - max) (every thread; K is small)
-  double lmax = -1e300;
-  for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
-  double zr = 0.0, zi = 0.0;
-  for (int k = 0; k < K; ++k) {
-    const double mag = exp((double)ell0[k].re - lmax);
-    zr += mag * cos((double)ell0[k].im);
-    zi += mag * sin((double)ell0[k].im);
-  }
-  const double zz = zr * zr + zi * zi;
-  auto pk = [&](int k, double& pr, double& pi_) {
-    const double mag = exp((double)ell0[k].re - lmax);
-    const double wr = mag * cos((double)ell0[k].im), wi = mag * sin((double)ell0[k].im);
-    pr = (wr * zr + wi * zi) / zz;
-    pi_ = (wi * zr - wr * zi) / zz;
+  energy_assembly(tid, N, n_up, M, K, Q, radius, lambda, interaction, b, x, jas, geo, dgeo, al, ell0, ellt, ellL,
+                  ellS, reinterpret_cast<double*>(sm + L.asmb), e_l, obs);
+}
+
+
+// ------------------------------------------------------------------ energy kernel, wave form
+// Round 5, N <= 8 (every entry of an N x N matrix has its own lane) with staged rows: ONE
+// 64-lane wave per walker (one-wave workgroups, so a barrier is a wave barrier), two phases
+// instead of det_energy_kernel's 17 barrier-separated channel rounds on 256 threads:
+//  (1) contraction.  The N orbital rows of channel c (each the electron's own spin block,
+//      RW = 2 M N K floats) stream HBM -> registers (float4, issued one channel ahead, while
+//      channel c - 1 is contracted) -> LDS; lane (i, j) forms every harmonic sum it needs:
+//        c = 0         Phi0 = sum F0 e0, D0t / D0p = sum F0 de/dth | de/dph,
+//                      L0 = sum F0 LB(e), S0k = sum F0 e_flow2,k
+//        c = 1 + t     Phi_t = sum Ft e0 (+ D0t | D0p on the moved electron's row i_t),
+//                      At / Ap = sum Ft de/dth | de/dph:  Gu_k += alpha_kt (phh_k At - thh_k Ap),
+//                      LB2 += At | Ap on row i_t
+//        c = 1 + T     Phi_L  = sum FL e0 + L0 + 2 LB2
+//        c = 2 + T + k Phi_Sk = sum FSk e0 + S0k + 2 Gu_k
+//      (det_energy_kernel's flow first-order sums sum F (phh_k de/dth - thh_k de/dph) are
+//      the same two harmonic sums At, Ap recombined: 3 complex sums per tangent channel
+//      instead of 5).  Phi_t goes to LDS, the other channel matrices stay in registers.
+//  (2) algebra.  B = Phi0^-1 by the same Gauss-Jordan (eliminate), M_t = B Phi_t with the
+//      column of Phi_t from LDS, tr M_t per t from LDS diagonals, the squared traces and the
+//      L / S traces as wave sums (the transposed entry by a lane permute), then the shared
+//      f64 assembly.  Same formulas as det_energy_kernel; the harmonic
+//      sums are the same FMAs in the same order, the extra terms are added as separate sums.
+// NV: float4 (VEC) or floats per lane per channel row set (N RW floats over 64 lanes).
+struct DetWaveSmem {
+  int S, LS, Fs, leaf, leaf2, Aug, fac, DG, geo, alpha, dgeo, asmb, ell, misc, total;
+};
+__host__ __device__ inline DetWaveSmem det_wave_layout(int N, int M, int K) {
+  DetWaveSmem L;
+  const int T = 2 * N, NN = N * N, RW = 2 * M * N * K, NK = N * K;
+  // staged row stride S = RW + pad with S = N K (mod 32): lane (i, j) reads bank K (i N + j)
+  // (conflict-free for K = 1); kept even so that a float4 lands as two 8-B stores
+  int want = NK & 31;
+  if (NK & 1) want = (want + 1) & 31;
+  L.S = RW + (((want - RW) % 32) + 32) % 32;
+  L.LS = 8 * M + 4;  // leaf row stride per electron: b128 reads of different electrons on different banks
+  int o = 0;
+  L.Fs = o;
+  o += N * L.S;
+  o = (o + 3) & ~3;
+  L.leaf = o;  // [i][m] (e0, de/dth, de/dph, d2e/dth2)
+  o += N * L.LS;
+  L.leaf2 = o;  // [i][m] (LB(e), e_flow2,0..2) for channel 0; then Phi_t [T][NN]
+  o += (N * L.LS > 2 * T * NN) ? N * L.LS : 2 * T * NN;
+  L.Aug = o;
+  o += 4 * NN;
+  L.fac = o;
+  o += 2 * N;
+  L.DG = o;
+  o += 2 * T * N;
+  L.geo = o;
+  o += 4 * N;
+  L.alpha = o;
+  o += 3 * T;
+  o = (o + 1) & ~1;
+  L.dgeo = o;
+  o += 8 * N;
+  L.asmb = o;
+  o += 2 * (4 * T + 3 * N);
+  L.ell = o;  // ell0 [K], ellt [K T], ellL [K], ellS [3 K] (complex)
+  o += 2 * K * (T + 5);
+  L.misc = o;
+  o += 8;
+  L.total = o;
+  return L;
+}
+constexpr int kDetWaveMaxN = 8;
+
+template <int NV, bool VEC>
+__global__ __launch_bounds__(64) void det_energy_wave_kernel(const float* __restrict__ Fp, int ldF,
+                                                             const float* __restrict__ x, const float* __restrict__ geo_g,
+                                                             const float* __restrict__ jas, const float* __restrict__ norm,
+                                                             float* __restrict__ e_l, float* __restrict__ obs, int N,
+                                                             int n_up, int M, int K, float Q, float radius, float lambda,
+                                                             int interaction) {
+  extern __shared__ float sm[];
+  const int T = 2 * N, C = 2 * N + 5, NN = N * N, NK = N * K, MNK = M * NK, RW = 2 * MNK;
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const DetWaveSmem L = det_wave_layout(N, M, K);
+  const int S = L.S, LS = L.LS;
+  float* Fs = sm + L.Fs;
+  float* leaf = sm + L.leaf;
+  float* leaf2 = sm + L.leaf2;
+  cf* Pt = reinterpret_cast<cf*>(sm + L.leaf2);  // after channel 0
+  cf* Aug = reinterpret_cast<cf*>(sm + L.Aug);
+  cf* fac = reinterpret_cast<cf*>(sm + L.fac);
+  cf* DG = reinterpret_cast<cf*>(sm + L.DG);
+  float* geo = sm + L.geo;
+  float* al = sm + L.alpha;
+  double* dgeo = reinterpret_cast<double*>(sm + L.dgeo);
+  cf* ell0 = reinterpret_cast<cf*>(sm + L.ell);
+  cf* ellt = ell0 + K;
+  cf* ellL = ellt + K * T;
+  cf* ellS = ellL + K;
+  int* piv = reinterpret_cast<int*>(sm + L.misc);
+  cf* logdet = reinterpret_cast<cf*>(sm + L.misc + 2);
+  // lane (i, j): entry (i, j) of every N x N matrix (lanes >= N N carry zeros)
+  const bool act = tid < NN;
+  const int i = act ? tid / N : 0, j = act ? tid - (tid / N) * N : 0;
+  const int tr_lane = j * N + i;  // the lane holding entry (j, i)
+
+  // ---- staging: channel c's N rows (own spin block) -> registers -> LDS (row stride S)
+  const size_t rowbase = (size_t)b * N * C;
+  using PF = typename std::conditional<VEC, float4, float>::type;
+  PF pf[NV];
+  const int unit = VEC ? 4 : 1, RU = RW / unit;  // units per row
+  auto stage_load = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int q = tid + 64 * u;
+      if (q < N * RU) {
+        const int r = q / RU, w = q - r * RU;
+        const int blk = (r >= n_up && n_up > 0) ? 1 : 0;
+        const float* src = Fp + (rowbase + (size_t)r * C + c) * ldF + (size_t)blk * RW + (size_t)w * unit;
+        if constexpr (VEC)
+          pf[u] = *reinterpret_cast<const float4*>(src);
+        else
+          pf[u] = *src;
+      }
+    }
   };
-  const double ap = jas[0], aa = jas[1];
-  if (tid < T) {
-    const int t = tid, i = t >> 1;
-    double gr = 0.0, gi = 0.0, sr = 0.0, si = 0.0;
-    for (int k = 0; k < K; ++k) {
-      double pr, pi_;
-      pk(k, pr, pi_);
-      const double lr = ellt[k * T + t].re, li = ellt[k * T + t].im;
-      gr += pr * lr - pi_ * li;
-      gi += pr * li + pi_ * lr;
-      const double l2r = lr * lr - li * li, l2i = 2.0 * lr * li;
-      sr += pr * l2r - pi_ * l2i;
-      si += pr * l2i + pi_ * l2r;
+  auto stage_store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int q = tid + 64 * u;
+      if (q < N * RU) {
+        const int r = q / RU, w = q - r * RU;
+        float* dst = Fs + r * S + w * unit;
+        if constexpr (VEC) {
+          reinterpret_cast<float2*>(dst)[0] = make_float2(pf[u].x, pf[u].y);
+          reinterpret_cast<float2*>(dst)[1] = make_float2(pf[u].z, pf[u].w);
+        } else {
+          *dst = pf[u];
+        }
+      }
     }
-    lbr[t] = sr - (gr * gr - gi * gi);
-    lbi[t] = si - 2.0 * gr * gi;
-    // Jastrow gradient along the (scaled) tangent t of electron i
-    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
-    const double ri[3] = {sti * cpi, sti * spi, cti};
-    const double et[3] = {(t & 1) ? -spi : cti * cpi, (t & 1) ? cpi : cti * spi, (t & 1) ? 0.0 : -sti};
-    double jg = 0.0;
-    for (int j = 0; j < N; ++j) {
-      if (j == i) continue;
-      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
-      const double rj[3] = {stj * cpj, stj * spj, ctj};
-      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
-      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
-      const bool same = (i < n_up) == (j < n_up);
-      double f1, f2;
-      (void)jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
-      jg += (-f1 / r) * (rj[0] * et[0] + rj[1] * et[1] + rj[2] * et[2]);
-    }
-    // gauge term A = i sum_i kappa_i phi_i (env_leaf) on the phi tangent
-    if (t & 1) gi += (double)env_gauge(geo[4 * i + 1], M) / sti;  // the leaves' kappa
-    tgr[t] = gr + jg;
-    tgi[t] = gi;
-  } else if (tid < T + N) {
-    const int i = tid - T;
-    const double sti = dgeo[4 * i], cti = dgeo[4 * i + 1], spi = dgeo[4 * i + 2], cpi = dgeo[4 * i + 3];
-    const double ri[3] = {sti * cpi, sti * spi, cti};
-    double J = 0.0, Jlb = 0.0, pe = 0.0;
-    for (int j = i + 1; j < N; ++j) {
-      const double stj = dgeo[4 * j], ctj = dgeo[4 * j + 1], spj = dgeo[4 * j + 2], cpj = dgeo[4 * j + 3];
-      const double rj[3] = {stj * cpj, stj * spj, ctj};
-      const double u = ri[0] * rj[0] + ri[1] * rj[1] + ri[2] * rj[2];
-      const double r = sqrt(fmax(2.0 - 2.0 * u, 0.0));
-      const bool same = (i < n_up) == (j < n_up);
-      double f1, f2;
-      J += jastrow_pair(r, same ? ap : aa, same ? 0.25 : 0.5, &f1, &f2);
-      Jlb += 2.0 * ((4.0 - r * r) * r * f2 + (4.0 - 3.0 * r * r) * f1) / (4.0 * r);
-      if (interaction == DH_INTERACTION_COULOMB)
-        pe += 1.0 / sqrt(2.0 - 2.0 * u);
-      else
-        pe += 1.0 + ((double)Q + 1.0) / (double)Q * u;
-    }
-    Jn[i] = J;
-    Jlbn[i] = Jlb;
-    pen[i] = pe;
+  };
+
+  // ---- geometry, flow coefficients (as det_energy_kernel)
+  for (int e = tid; e < N; e += 64) {
+    const float4 g = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + e));
+    geo[4 * e] = g.x;
+    geo[4 * e + 1] = g.y;
+    geo[4 * e + 2] = g.z;
+    geo[4 * e + 3] = g.w;
+    double st, ct, sp, cp;
+    sincos((double)x[2 * (b * N + e)], &st, &ct);
+    sincos((double)x[2 * (b * N + e) + 1], &sp, &cp);
+    dgeo[4 * e] = st;
+    dgeo[4 * e + 1] = ct;
+    dgeo[4 * e + 2] = sp;
+    dgeo[4 * e + 3] = cp;
   }
   __syncthreads();
-  if (tid == 0) {
-    const double val_re = 0.5 * log(zz) + lmax, val_im = atan2(zi, zr);
-    double LB_re = 0.0, LB_im = 0.0;
-    for (int k = 0; k < K; ++k) {
-      double pr, pi_;
-      pk(k, pr, pi_);
-      LB_re += pr * ellL[k].re - pi_ * ellL[k].im;
-      LB_im += pr * ellL[k].im + pi_ * ellL[k].re;
+  for (int t = tid; t < T; t += 64) {
+    const int e = t >> 1;
+    const float st = geo[4 * e], ct = geo[4 * e + 1], sp = geo[4 * e + 2], cp = geo[4 * e + 3];
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((t & 1) == 0)
+        a = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+      else
+        a = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+      al[k * T + t] = a;
     }
-    for (int t = 0; t < T; ++t) {
-      LB_re += lbr[t];
-      LB_im += lbi[t];
-    }
-    double S_re[3], S_im[3];
-#pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-      double a_r = 0.0, a_i = 0.0, m1r = 0.0, m1i = 0.0, m2r = 0.0, m2i = 0.0;
-      for (int k = 0; k < K; ++k) {
-        double pr, pi_;
-        pk(k, pr, pi_);
-        a_r += pr * ellS[3 * k + kk].re - pi_ * ellS[3 * k + kk].im;
-        a_i += pr * ellS[3 * k + kk].im + pi_ * ellS[3 * k + kk].re;
-        double gur = 0.0, gui = 0.0;
-        for (int t = 0; t < T; ++t) {
-          gur += (double)al[kk * T + t] * ellt[k * T + t].re;
-          gui += (double)al[kk * T + t] * ellt[k * T + t].im;
-        }
-        m1r += pr * gur - pi_ * gui;
-        m1i += pr * gui + pi_ * gur;
-        const double g2r = gur * gur - gui * gui, g2i = 2.0 * gur * gui;
-        m2r += pr * g2r - pi_ * g2i;
-        m2i += pr * g2i + pi_ * g2r;
-      }
-      S_re[kk] = a_r + m2r - (m1r * m1r - m1i * m1i);
-      S_im[kk] = a_i + m2i - 2.0 * m1r * m1i;
-    }
-    double J = 0.0, Jlb = 0.0, pe = 0.0;
-    for (int i = 0; i < N; ++i) {
-      J += Jn[i];
-      Jlb += Jlbn[i];
-      pe += pen[i];
-    }
-    if (interaction == DH_INTERACTION_COULOMB) pe /= (double)radius;
-    // gauge terms: phase and the flow channels' phi acceleration (see env_flow2)
-    double gauge_phase = 0.0;
-    for (int i = 0; i < N; ++i) {
-      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
-      const double kap = (double)env_gauge(geo[4 * i + 1], M);  // the leaves' kappa
-      gauge_phase += kap * (double)x[2 * (b * N + i) + 1];
-      const double cot = ct / st;
-      const double tdot[3] = {-sp, cp, 0.0};
-      const double thp[3] = {cp * cot, sp * cot, -1.0};
-      const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
-      const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 3; ++kk) S_im[kk] += kap * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
-    }
-    pe *= (double)lambda;
-    LB_re += Jlb;
-    double sq_re = 0.0, sq_im = 0.0, mag_re = 0.0, mag_im = 0.0;
-    for (int t = 0; t < T; ++t) {
-      sq_re += tgr[t] * tgr[t] - tgi[t] * tgi[t];
-      sq_im += 2.0 * tgr[t] * tgi[t];
-    }
-    double Mv[3] = {0.0, 0.0, 0.0};
-    for (int i = 0; i < N; ++i) {
-      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
-      const double cot = ct / st;
-      mag_re += (Q * cot) * (Q * cot);
-      mag_re += -2.0 * Q * cot * tgi[2 * i + 1];  // 2 i Q cot * t_phi_scaled
-      mag_im += 2.0 * Q * cot * tgr[2 * i + 1];
-      Mv[0] += Q * cp / st;
-      Mv[1] += Q * sp / st;
-    }
-    const double r2 = (double)radius * radius;
-    const double ke_re = (-LB_re - sq_re + mag_re) / (2.0 * r2);
-    const double ke_im = (-LB_im - sq_im + mag_im) / (2.0 * r2);
-    double G_re[3], G_im[3];
-#pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-      double gr = 0.0, gi = 0.0;
-      for (int t = 0; t < T; ++t) {
-        gr += (double)al[kk * T + t] * tgr[t];
-        gi += (double)al[kk * T + t] * tgi[t];
-      }
-      G_re[kk] = gr;
-      G_im[kk] = gi;
-    }
-    double L2 = 0.0;
-#pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-      const double ar = G_re[kk], ai = G_im[kk] + Mv[kk];  // (G + i M)^2, real part
-      L2 -= S_re[kk] + (ar * ar - ai * ai);
-    }
-    const double lz = G_im[2];
-    const double lz2 = -(S_re[2] + G_re[2] * G_re[2] - G_im[2] * G_im[2]);
-    e_l[2 * b] = (float)(ke_re + pe);
-    e_l[2 * b + 1] = (float)ke_im;
-    float* ob = obs + 8 * (size_t)b;
-    ob[0] = (float)ke_re;
-    ob[1] = (float)ke_im;
-    ob[2] = (float)pe;
-    ob[3] = (float)lz;
-    ob[4] = (float)lz2;
-    ob[5] = (float)L2;
-    ob[6] = (float)(val_re + J);
-    ob[7] = (float)remainder(val_im + gauge_phase, 2.0 * M_PI);
   }
+  // this lane's row geometry (flow first-order coefficients phh, thh of electron i)
+  const float gst = geo[4 * i], gct = geo[4 * i + 1], gsp = geo[4 * i + 2], gcp = geo[4 * i + 3];
+  const float phh[3] = {-gsp, gcp, 0.f};
+  const float thh[3] = {gct * gcp, gct * gsp, -gst};
+
+  for (int kd = 0; kd < K; ++kd) {
+    stage_load(0);
+    // envelope leaves of every (electron, harmonic): e0, de/dth, de/dph, d2e/dth2 and, for
+    // channel 0, LB(e) and the flow second derivatives (same functions as det_energy_kernel)
+    __syncthreads();  // Pt of the previous determinant (aliases leaf2) is consumed
+    for (int idx = tid; idx < N * M; idx += 64) {
+      const int e = idx / M, p = idx - (idx / M) * M;
+      const float st = geo[4 * e], ct = geo[4 * e + 1], sp = geo[4 * e + 2], cp = geo[4 * e + 3];
+      const float gauge = env_gauge(ct, M);
+      const EnvLeaf lf = env_leaf(x[2 * (b * N + e)], x[2 * (b * N + e) + 1], p, M, norm[p], true, gauge);
+      const float m = (float)p - 0.5f * (float)(M - 1) - gauge;
+      float* d = leaf + e * LS + 8 * p;
+      reinterpret_cast<float4*>(d)[0] = make_float4(lf.e0.re, lf.e0.im, lf.dth.re, lf.dth.im);
+      reinterpret_cast<float4*>(d)[1] = make_float4(lf.dph.re, lf.dph.im, lf.d2th.re, lf.d2th.im);
+      const cf f0 = env_flow2(lf.e0, lf.dth, lf.d2th, m, st, ct, sp, cp, 0);
+      const cf f1 = env_flow2(lf.e0, lf.dth, lf.d2th, m, st, ct, sp, cp, 1);
+      const cf f2 = env_flow2(lf.e0, lf.dth, lf.d2th, m, st, ct, sp, cp, 2);
+      float* d2 = leaf2 + e * LS + 8 * p;
+      reinterpret_cast<float4*>(d2)[0] = make_float4(lf.lb.re, lf.lb.im, f0.re, f0.im);
+      reinterpret_cast<float4*>(d2)[1] = make_float4(f1.re, f1.im, f2.re, f2.im);
+    }
+    const float* Frow = Fs + i * S + j * K + kd;  // re at + m NK, im at + MNK + m NK
+    const float* lrow = leaf + i * LS;
+    const float* l2row = leaf2 + i * LS;
+    cf P0{0.f, 0.f}, D0t{0.f, 0.f}, D0p{0.f, 0.f}, L0{0.f, 0.f}, S0[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    cf Gu[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}}, LB2{0.f, 0.f}, PL{0.f, 0.f};
+    cf PS[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    for (int c = 0; c < C; ++c) {
+      __syncthreads();  // the readers of channel c - 1 are done with Fs
+      stage_store();
+      __syncthreads();
+      if (c + 1 < C) stage_load(c + 1);  // in flight while channel c is contracted
+      if (c == 0) {
+        for (int m = 0; m < M; ++m) {
+          const cf f{Frow[m * NK], Frow[MNK + m * NK]};
+          const float4 a = *reinterpret_cast<const float4*>(lrow + 8 * m);
+          const float4 q = *reinterpret_cast<const float4*>(lrow + 8 * m + 4);
+          const float4 u = *reinterpret_cast<const float4*>(l2row + 8 * m);
+          const float4 v = *reinterpret_cast<const float4*>(l2row + 8 * m + 4);
+          cfma(P0, f, cf{a.x, a.y});
+          cfma(D0t, f, cf{a.z, a.w});
+          cfma(D0p, f, cf{q.x, q.y});
+          cfma(L0, f, cf{u.x, u.y});
+          cfma(S0[0], f, cf{u.z, u.w});
+          cfma(S0[1], f, cf{v.x, v.y});
+          cfma(S0[2], f, cf{v.z, v.w});
+        }
+      } else if (c <= T) {
+        const int t = c - 1;
+        cf Pe{0.f, 0.f}, At{0.f, 0.f}, Ap{0.f, 0.f};
+#pragma unroll 4
+        for (int m = 0; m < M; ++m) {
+          const cf f{Frow[m * NK], Frow[MNK + m * NK]};
+          const float4 a = *reinterpret_cast<const float4*>(lrow + 8 * m);
+          const float2 q = *reinterpret_cast<const float2*>(lrow + 8 * m + 4);
+          cfma(Pe, f, cf{a.x, a.y});
+          cfma(At, f, cf{a.z, a.w});
+          cfma(Ap, f, cf{q.x, q.y});
+        }
+        const bool own = (i == (t >> 1));
+        if (own) {
+          Pe += (t & 1) ? D0p : D0t;
+          LB2 += (t & 1) ? Ap : At;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float ak = al[k * T + t];
+          const cf g{phh[k] * At.re - thh[k] * Ap.re, phh[k] * At.im - thh[k] * Ap.im};
+          Gu[k] += ak * g;
+        }
+        if (act) Pt[t * NN + tid] = Pe;  // leaf2 is free: channel 0's readers passed the barriers above
+      } else {
+        cf Pe{0.f, 0.f};
+#pragma unroll 4
+        for (int m = 0; m < M; ++m) {
+          const cf f{Frow[m * NK], Frow[MNK + m * NK]};
+          const float2 a = *reinterpret_cast<const float2*>(lrow + 8 * m);
+          cfma(Pe, f, cf{a.x, a.y});
+        }
+        // (register arrays indexed by compile-time constants only: a run-time index sends them to scratch)
+        if (c == T + 1)
+          PL = Pe + L0 + 2.f * LB2;
+        else if (c == T + 2)
+          PS[0] = Pe + S0[0] + 2.f * Gu[0];
+        else if (c == T + 3)
+          PS[1] = Pe + S0[1] + 2.f * Gu[1];
+        else
+          PS[2] = Pe + S0[2] + 2.f * Gu[2];
+      }
+    }
+    // ---- B = Phi0^-1 (augmented Gauss-Jordan, partial pivoting), log det Phi0
+    if (act) {
+      Aug[i * 2 * N + j] = P0;
+      Aug[i * 2 * N + N + j] = (i == j) ? cf{1.f, 0.f} : cf{0.f, 0.f};
+    }
+    __syncthreads();
+    eliminate(Aug, 2 * N, N, 2 * N, true, fac, piv, logdet, tid, 64, 64);
+    if (tid == 0) ell0[kd] = *logdet;
+    cf Br[kDetWaveMaxN];
+#pragma unroll
+    for (int l = 0; l < kDetWaveMaxN; ++l) Br[l] = (act && l < N) ? Aug[i * 2 * N + N + l] : cf{0.f, 0.f};
+    const cf BT = act ? Aug[j * 2 * N + N + i] : cf{0.f, 0.f};  // B[j][i]
+    // ---- M_t = B Phi_t, traces
+    cf sq{0.f, 0.f}, Mu[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    for (int t = 0; t < T; ++t) {
+      cf mt{0.f, 0.f};
+#pragma unroll
+      for (int l = 0; l < kDetWaveMaxN; ++l)
+        if (l < N) cfma(mt, Br[l], act ? Pt[t * NN + l * N + j] : cf{0.f, 0.f});
+      const cf mT{__shfl(mt.re, tr_lane, 64), __shfl(mt.im, tr_lane, 64)};
+      if (act) {
+        sq += mt * mT;
+        if (i == j) DG[t * N + i] = mt;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Mu[k] += al[k * T + t] * mt;
+    }
+    float v[16];
+    {
+      const cf pl = act ? BT * PL : cf{0.f, 0.f};
+      v[0] = sq.re;
+      v[1] = sq.im;
+      v[2] = pl.re;
+      v[3] = pl.im;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const cf ps = act ? BT * PS[k] : cf{0.f, 0.f};
+        const cf muT{__shfl(Mu[k].re, tr_lane, 64), __shfl(Mu[k].im, tr_lane, 64)};
+        const cf m2 = act ? Mu[k] * muT : cf{0.f, 0.f};
+        v[4 + 4 * k] = ps.re;
+        v[5 + 4 * k] = ps.im;
+        v[6 + 4 * k] = m2.re;
+        v[7 + 4 * k] = m2.im;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = wave_sum(v[q]);
+    __syncthreads();  // DG written
+    if (tid < T) {
+      cf s{0.f, 0.f};
+      for (int e = 0; e < N; ++e) s += DG[tid * N + e];
+      ellt[kd * T + tid] = s;
+    }
+    if (tid == 0) {
+      ellL[kd] = cf{v[2] - v[0], v[3] - v[1]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ellS[3 * kd + k] = cf{v[4 + 4 * k] - v[6 + 4 * k], v[5 + 4 * k] - v[7 + 4 * k]};
+    }
+  }
+  energy_assembly(tid, N, n_up, M, K, Q, radius, lambda, interaction, b, x, jas, geo, dgeo, al, ell0, ellt, ellL, ellS,
+                  reinterpret_cast<double*>(sm + L.asmb), e_l, obs);
 }
 
 
@@ -1444,8 +1784,58 @@ bool det_precontract(const Dims& d) {
   return fits && !(det_staged(d.N, d.M, d.K) && 2 * d.M * d.N * d.K * d.N <= 8 * 256);
 }
 
+// DH_DET_V2=0 keeps det_energy_kernel for the staged (N <= 8) shapes (A/B measurements)
+static bool det_wave_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_DET_V2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// det_energy_wave_kernel for this shape: the template's per-lane staging width NV, or 0
+static int det_wave_nv(const Dims& d, bool& vec) {
+  if (d.N > kDetWaveMaxN || !det_staged(d.N, d.M, d.K)) return 0;
+  const int RW = 2 * d.M * d.N * d.K;
+  vec = (RW % 4 == 0) && (d.ld_orb % 4 == 0);
+  const int units = vec ? d.N * RW / 4 : d.N * RW;
+  const int need = (units + 63) / 64;
+  for (int v : (vec ? std::initializer_list<int>{1, 2, 3, 5, 8, 12} : std::initializer_list<int>{1, 2, 4, 8, 16}))
+    if (need <= v) return v;
+  return 0;
+}
+
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic) {
+  bool vec = false;
+  const int nv = phic ? 0 : det_wave_nv(d, vec);
+  if (nv > 0 && det_wave_enabled()) {
+    const size_t bytes = (size_t)det_wave_layout(d.N, d.M, d.K).total * sizeof(float);
+    auto go = [&](auto kern) {
+      ensure_smem(kern, bytes);
+      hipLaunchKernelGGL(kern, dim3(nw), dim3(64), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N, d.n_up,
+                         d.M, d.K, d.Q, d.r, d.lambda, d.interaction);
+    };
+    if (vec) {
+      switch (nv) {
+        case 1: go(det_energy_wave_kernel<1, true>); break;
+        case 2: go(det_energy_wave_kernel<2, true>); break;
+        case 3: go(det_energy_wave_kernel<3, true>); break;
+        case 5: go(det_energy_wave_kernel<5, true>); break;
+        case 8: go(det_energy_wave_kernel<8, true>); break;
+        default: go(det_energy_wave_kernel<12, true>); break;
+      }
+    } else {
+      switch (nv) {
+        case 1: go(det_energy_wave_kernel<1, false>); break;
+        case 2: go(det_energy_wave_kernel<2, false>); break;
+        case 4: go(det_energy_wave_kernel<4, false>); break;
+        case 8: go(det_energy_wave_kernel<8, false>); break;
+        default: go(det_energy_wave_kernel<16, false>); break;
+      }
+    }
+    return;
+  }
   // DH_DET_WAVE=1: one wave per walker (measured slower: C2 0.60 -> 1.21 ms per step, C5
   // 13.0 -> 14.0 ms; the per-walker work, not the barriers, dominates — DESIGN.md §7.1)
   static const bool wave_mode = [] {

@@ -25,6 +25,7 @@ struct Dims {
   int sparse;          // orbital type "sparse": F = 8 features per (j, k) (blocks.py:52-62)
 };
 constexpr int kSparseFeatures = 8;
+constexpr int kMqkStride = 32;  // floats per head of layer 1's score forms Mqk (25 used; attn_val.h)
 
 // Device pointers into the packed parameter buffer.
 struct LayerParams {
@@ -45,6 +46,7 @@ struct Params {
   const uint16_t* WorbP;  // split-bf16 planes of Worb
   const uint16_t* WorbB;  // backward planes (untransposed Worb [D][ld_orb])
   const float* WorbBT;    // backward exact-f32 copy Worb^T [ld_orb][D]
+  const float* Mqk;       // layer 1's score forms Wq~ Wk~^T / 8, [H][kMqkStride] (attn_val.h)
 };
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
@@ -111,6 +113,7 @@ struct X6Feat {
   // (folded W0 Wqkv [4][3D], bqkv [3D]) instead of read from X1 (chain_attn_supported)
   const float* W0qkv = nullptr;
   const float* bqkv = nullptr;
+  const float* Mqk = nullptr;  // [H][kMqkStride] (attn_val.h attn_feat_core)
 };
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});
@@ -165,7 +168,10 @@ bool attention_mfma_supported(const Dims& d);
 void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s,
                            const float* W0qkv, const float* bqkv);
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
-                      const float* W0qkv = nullptr, const float* bqkv = nullptr);
+                      const float* W0qkv = nullptr, const float* bqkv = nullptr, const float* Mqk = nullptr);
+// layer 1's 5 x 5 score forms per head, Mqk[h][a][b] = sum_d Wq~[a][h dh + d] Wk~[b][h dh + d] / 8
+// (Wq~ / Wk~ = the folded W0 Wqkv rows with the bias as row 4; dh = 64; f64 sums)
+void launch_lowrank_qk(const Dims& d, const float* W0qkv, const float* bqkv, float* Mqk, hipStream_t s);
 
 // layernorm.hip
 //   mode 0: h = LN_ch(X)           (X may alias h)

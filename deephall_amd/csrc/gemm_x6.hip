@@ -2234,9 +2234,10 @@ __device__ __forceinline__ void split4(const float4& x, uint2& h, uint2& m, uint
 
 // NA > 0: layer 1 with its attention fused (X1 unused): the prologue forms o of the tile's
 // 96 / NA walkers itself (attn_val.h, bit-identical to attention_val_kernel<NA, true>): wave
-// w takes head w % 4 for walkers 48 / NA * (w / 4) .., two walkers per attn_val_core call
-// so their LDS round trips overlap, staging q / k in LDS that the planes
-// overwrite afterwards, the o values held in registers (48 per lane) until every wave is done.
+// w takes head w % 4 for walkers 48 / NA * (w / 4) .., two walkers per attn_feat_core call
+// so their LDS round trips overlap (round 5: the scores from the features through the head's
+// 5 x 5 form Mqk, no q / k rows), staging the weights in LDS that the planes overwrite
+// afterwards, the o values held in registers (48 per lane) until every wave is done.
 template <int ABLS = 0, int NA = 0>  // ABLS (tools only): 1 weight fragments from one k-tile (L1-resident); 2 no P3 stores
 __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
@@ -2406,23 +2407,26 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     const int hd = wid & 3, wl0 = (wid >> 2) * WPW;  // head; first tile walker of this wave
     FeatW fw;
     fw.load(a.feat.W0qkv, a.feat.bqkv, CH_K, hd * 64 + lane);
+    const float* Mh = a.feat.Mqk + hd * kMqkStride;  // the head's score form (attn_feat_core)
     float ov[WPW][NA];
     // the wave-uniform guards also keep the scheduler from hoisting later walkers' loads (spills)
 #pragma unroll
     for (int t = 0; t < WPW; t += ANT) {
       const int b = row0 / NA + wl0 + t;
       if ((b + ANT) * NA <= rows) {
-        float pq[ANT][NA], pk[ANT][NA], pv[ANT][NA];
+        float pv[ANT][NA];
 #pragma unroll
-        for (int u = 0; u < ANT; ++u) feat_qkv<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pq[u], pk[u], pv[u]);
-        attn_val_core<NA, ANT>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
+        for (int u = 0; u < ANT; ++u) feat_v<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pv[u]);
+        attn_feat_core<NA, ANT>(Mh, a.feat.geo, b, a.feat.n_up, pv, qs, lane,
+                                reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
       } else {  // the batch ends inside this group (last tile)
 #pragma unroll
         for (int u = 0; u < ANT; ++u) {
           if ((b + u + 1) * NA <= rows) {
-            float pq[1][NA], pk[1][NA], pv[1][NA];
-            feat_qkv<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pq[0], pk[0], pv[0]);
-            attn_val_core<NA, 1>(pq, pk, pv, qs, lane, reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
+            float pv[1][NA];
+            feat_v<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pv[0]);
+            attn_feat_core<NA, 1>(Mh, a.feat.geo, b + u, a.feat.n_up, pv, qs, lane,
+                                  reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
           } else {
 #pragma unroll
             for (int i = 0; i < NA; ++i) ov[t + u][i] = 0.f;

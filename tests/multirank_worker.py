@@ -67,6 +67,8 @@ def main_train(out, world, rank, run_dir):
 
 def main_kfac(out, world, rank):
     from deephall_amd import Config, make_network
+    from deephall_amd.loss import _kfac_buffer
+    from deephall_amd.mcmc import resolve_network
     from deephall_amd.loss import LossMode, make_loss_fn
     from deephall_amd.optimizers import make_optimizer_step
     from deephall_amd.types import CheckpointState
@@ -101,16 +103,89 @@ def main_kfac(out, world, rank):
     init, step = make_optimizer_step(cfg, model)
     state = CheckpointState(params, x, init(params), 0.1)
     p0 = params.flat.clone()
-    snaps, pgs = [], []
+    snaps, pgs, inputs = [], [], []
     for _ in range(2):
         state, _ = step(state)
         snaps.append(state.params.flat.clone())
         pgs.append(state.opt_state.pgrad.clone())
+        # the step's all-reduced [gradient | curvature statistics] (the loss fn's cached buffer)
+        buf, nref = _kfac_buffer(resolve_network(model), x.device)
+        inputs.append(buf.clone())
     torch.cuda.synchronize()
+    if world > 1 and rank == 0:
+        extra.update(_kfac_oracle_two_steps(model, cfg, p0, snaps[0], inputs, nref, world, B))
     np.savez(f"{out}_{rank}.npz", grad=g0.cpu().numpy(), curv=curv.cpu().numpy(), p0=p0.cpu().numpy(),
              p1=snaps[0].cpu().numpy(), p2=snaps[1].cpu().numpy(), pg1=pgs[0].cpu().numpy(),
              pg2=pgs[1].cpu().numpy(), info=state.opt_state.info.cpu().numpy(), gmask=gmask.cpu().numpy(),
              energy=complex(stats["energy"].item()), **extra)
+
+
+def _kfac_oracle_two_steps(model, cfg, p0, p1, inputs, nref, world, B):
+    """the two-rank run's two KFAC steps against oracle/kfac.py fed the
+    SAME per-step inputs — each step's all-reduced gradient and curvature statistics, as the
+    ranks hold them — with float32 EMA storage (as tests/test_gpu_kfac.py).  Also the oracle's
+    own two-shard statistics (kfac_jax multi_device: per-device statistics, averaged) at the
+    step-2 parameters, against the statistics the ranks all-reduced there.  Returns the
+    oracle's P g / parameters per step and the statistics' relative errors."""
+    from deephall_amd.networks.psiformer import ParamTree
+    from helpers import make_walkers
+    from oracle import kfac as KF
+    from oracle import reference as R
+
+    ocfg = R.OracleConfig(nspins=tuple(cfg.system.nspins), flux=cfg.system.flux,
+                          num_heads=cfg.network.psiformer.num_heads, heads_dim=cfg.network.psiformer.heads_dim,
+                          num_layers=cfg.network.psiformer.num_layers)
+    lay = model.kfac_layout(p0.device)
+    blocks, generic = KF.blocks(ocfg)
+    assert len(blocks) == len(lay["blocks"])
+
+    def tree(flat):
+        t = ParamTree.view_of(model.spec, flat.to(p0.device))
+        return {k: t[k].double().cpu() for k in t}
+
+    def unpack(curv):
+        curv = curv.double().cpu()
+        stats = {}
+        for ob, gb in zip(blocks, lay["blocks"]):
+            (na, oa), (ng, og) = lay["slots"][gb["a_slot"]], lay["slots"][gb["g_slot"]]
+            stats[ob.name] = (curv[oa: oa + na * na].reshape(na, na), curv[og: og + ng * ng].reshape(ng, ng))
+        diag, o = {}, lay["nmat"]
+        shapes = tree(p0)
+        for g in generic:
+            n = shapes[g].numel()
+            diag[g] = curv[o: o + n].reshape(shapes[g].shape)
+            o += n
+        return stats, diag
+
+    ema = float(np.float32(0.95))  # the float32 EMA factor the kernels see
+    state = KF.KfacState()
+    p_ref = tree(p0)
+    res = {}
+    for s, buf in enumerate(inputs, start=1):
+        grads = tree(buf[:nref])
+        stats, diag = unpack(buf[nref:])
+        p_ref, state, inf = KF.kfac_step(p_ref, ocfg, grads, state, stats, diag, storage=torch.float32, ema=ema)
+        flat = ParamTree.zeros(model.spec, p0.device)
+        pgt = ParamTree.zeros(model.spec, p0.device)
+        for k in p_ref:
+            flat[k].copy_(p_ref[k].float().reshape(flat[k].shape))
+            pgt[k].copy_(inf["pg"][k].float().reshape(pgt[k].shape))
+        res[f"oracle_p{s}"] = flat.flat.cpu().numpy()
+        res[f"oracle_pg{s}"] = pgt.flat.cpu().numpy()
+        res[f"oracle_coef{s}"] = inf["coef"]
+    # the oracle's two-shard statistics at the parameters of step 2 (the ranks' step-1 result)
+    xs = torch.tensor(make_walkers(B, ocfg.nelec, seed=21), dtype=torch.float64)
+    ref, rdiag = KF.batch_statistics(tree(p1), ocfg, xs, shards=world)
+    got, gdiag = unpack(inputs[1][nref:])
+    errs = []
+    for k, (A, G) in ref.items():
+        errs.append(float((got[k][0] - A).abs().max() / A.abs().max()))
+        errs.append(float((got[k][1] - G).abs().max() / G.abs().max()))
+    gen_ref = torch.cat([rdiag[g].reshape(-1) for g in generic])
+    gen_got = torch.cat([gdiag[g].reshape(-1) for g in generic])
+    res["stat2_err_dense"] = max(errs)
+    res["stat2_err_generic"] = float((gen_got - gen_ref).abs().max() / gen_ref.abs().max())
+    return res
 
 
 def main_nccl(out):

@@ -6,9 +6,10 @@ fixture (tests/golden/make_golden.py, round2) holds the float64 restatement's va
 the same full-Hessian algorithm run in float32 on the same walkers and parameters.  Per
 observable the HIP errors (relative, floor 1) must sit at or below that float32 run's
 error distribution (helpers.within_f32_floor): median within 1.5x, 90th percentile
-within 2x, the single worst walker within 4x (6x for the near-pole fixtures: an ill-conditioned
-orbital matrix dominates it, and two independent f32 rounding draws differ there), 2e-7 slack; log psi and its phase pass
-outright when every walker is within 1e-5.  The fixtures cover near-pole walkers
+within 2x, the single worst walker within 4x on every fixture (helpers.FLOOR_X_MAX; one
+limit since round 4, near-pole fixtures included: an ill-conditioned orbital matrix sets the
+worst walker, and two independent f32 rounding draws differ there), 2e-7 slack; log psi and
+its phase pass outright when every walker is within 1e-5.  The fixtures cover near-pole walkers
 (theta in [1e-3, 0.15] and pi minus that), the harmonic potential, an explicit radius,
 and 32-walker batches at C2, C4 and C5.  Every test prints the per-observable max and
 median relative errors (HIP and f32 run) that DESIGN.md §5 tabulates.
