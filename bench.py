@@ -300,7 +300,7 @@ def main():
     # the other BASELINE.json configs with a larger N (configs[3] N=10 2Q=23, configs[4] N=20 2Q=57),
     # one-GPU weak-scaling lines of the same VMC iteration (4096 walkers per GPU), a few steps each
     extra = {}
-    if args.extra_configs:
+    if args.extra_configs and world == 1:  # one-GPU lines: not repeated by the multi-rank runs
         for tag in args.extra_configs.split(","):
             nsp, fx = EXTRA_CONFIGS[tag]
             rx = run_workload(args, dev, rank, world, nsp, fx, B, args.extra_steps, args.extra_warmup, 2,
@@ -375,7 +375,9 @@ def main():
             out["configs_1gpu"][tag] = {
                 "config": f"nspins={list(nsp)} flux={fx} (BASELINE.json configs[{3 if tag == 'C4' else 4}], "
                           f"{B} walkers per GPU, weak scaling)",
-                "value": round(B_total * args.extra_steps / rx["dt"], 1),
+                # a one-GPU line: this rank's walkers over the max-over-ranks time (B, not
+                # B_total: with --gpus > 1 the ranks run these configs side by side)
+                "value": round(B * args.extra_steps / rx["dt"], 1),
                 "unit": "local-energies/s",
                 "steps": args.extra_steps,
                 "warmup": args.extra_warmup,
@@ -385,7 +387,7 @@ def main():
                 "kernels_ms_per_step": {k: round(v["ms_per_step"], 3)
                                         for k, v in kernels_of(rx["prof"], args.extra_steps).items()},
                 "energy": [round(rx["energy"].real, 5), round(rx["energy"].imag, 5)],
-                "model_tflops_step": round(B_total * (2 * n + 5 + args.mcmc_steps + 1) * f_fwd(n, fx)
+                "model_tflops_step": round(B * (2 * n + 5 + args.mcmc_steps + 1) * f_fwd(n, fx)
                                            / rx["dt"] * args.extra_steps / 1e12, 2),
             }
     if world == 1 and not args.no_cpu_baseline:

@@ -1042,15 +1042,17 @@ int vjp_backward(dh_handle* h, const float* x, int nw, const float* ct, float* g
   };
   // KFAC Gram matrices: slot (+)= scale X^T X (n columns of X, row stride ldx, `nr` rows),
   // with the bias row / column / corner of [X, 1] when aug
-  auto gram = [&](const float* X, int ldx, int n, int slot, float scale, int nr, bool aug) {
+  // (accum: add to the slot instead of overwriting it; default kf->acc, the chunk loop's flag)
+  auto gram = [&](const float* X, int ldx, int n, int slot, float scale, int nr, bool aug, int accum = -1) {
     const KfacSlot& sl = kf->plan->slots[slot];
     float* out = kf->stats + sl.off;
     const int nc2 = grad_chunks(nr);
+    const int a = accum < 0 ? kf->acc : accum;
     launch_tn_partial(X, ldx, X, ldx, nr, n, n, w.P, s);
-    launch_reduce2d(w.P, nc2, (size_t)n * n, n, n, n, out, sl.n, scale, kf->acc, s);
+    launch_reduce2d(w.P, nc2, (size_t)n * n, n, n, n, out, sl.n, scale, a, s);
     if (aug) {
       launch_colsum_partial(X, ldx, nr, n, w.P, s);
-      launch_kfac_aug(w.P, nc2, n, out, sl.n, scale, (float)nr * scale, kf->acc, s);
+      launch_kfac_aug(w.P, nc2, n, out, sl.n, scale, (float)nr * scale, a, s);
     }
   };
   // ---- backward
@@ -1088,16 +1090,16 @@ int vjp_backward(dh_handle* h, const float* x, int nw, const float* ct, float* g
           }
           // the lll_weight input (the real featured orbitals h W + b, exact f32) in rows of 8,
           // its output tangent (the real feature segment) in rows of M; spin blocks accumulate
-          KfacAcc k2 = *kf;
-          k2.acc = kf->acc || blk > 0;
+          const int acc_lll = (kf->acc || blk > 0) ? 1 : 0;
           launch_gemm(hb, D, ref(RS.orb_kernel(2 * blk)), F8, ref(RS.orb_bias(2 * blk)), nullptr, 0, w.kfs1, F8, nr,
                       F8, D, 1, s);
-          const KfacAcc* keep = kf;
-          kf = &k2;
-          gram(w.kfs1, 8, 8, K.A_lll, inv_lll, nr * NK, false);
+          gram(w.kfs1, 8, 8, K.A_lll, inv_lll, nr * NK, false, acc_lll);
+          // scratch for the regrouped tangent: w.F, the saved orbital matrix of this chunk's
+          // forward — dead here, because this (Fisher) reverse pass is its last reader: the
+          // gradient pass ran first and this pass's launch_det_bwd above has consumed it; the
+          // next chunk's forward rewrites it.  dh_kfac_vjp must keep that order.
           launch_kfac_sparse_regroup(w.dF, d.ld_orb, d.M, NK, blk * 2, nr, nna, d.N, nlo, w.F, s);
-          gram(w.F, d.M, d.M, K.G_lll, inv_lll, nr * NK, false);
-          kf = keep;
+          gram(w.F, d.M, d.M, K.G_lll, inv_lll, nr * NK, false, acc_lll);
           // the generic lll bias tangent: sum over rows of the real feature segment
           launch_colsum_partial(w.F, d.M, nr * NK, d.M, w.P, s);
           launch_reduce2d(w.P, grad_chunks(nr * NK), (size_t)d.M, d.M, 1, d.M, g(RS.lll(1)), d.M, 1.f, acc || blk > 0,

@@ -207,16 +207,17 @@ class LogManager:
             if keys and opt_init is not None:
                 opt_state = opt_init(params)
                 if opt_state is not None:
-                    try:
+                    saved = {k.split("/", 1)[1] for k in keys}
+                    if saved != set(opt_state.state_dict()):
+                        # a different optimizer wrote the checkpoint (e.g. an Adam checkpoint
+                        # restored into a run with the KFAC default): keep the params, walkers
+                        # and step, start the optimizer state afresh
+                        logger.warning("Checkpoint %s: optimizer state keys %s do not match the current "
+                                       "optimizer's %s; params, walkers and step restored, optimizer state "
+                                       "re-initialised", path, sorted(saved), sorted(opt_state.state_dict()))
+                    else:
+                        # same optimizer: a wrong size or corrupt entry is an error, not a reset
                         opt_state.load_state_dict({k.split("/", 1)[1]: f[k] for k in keys})
-                    except (KeyError, ValueError, RuntimeError) as e:
-                        # the optimizer changed since the checkpoint was written (e.g. an Adam
-                        # checkpoint restored into a run with the KFAC default): keep the params,
-                        # walkers and step, start the optimizer state afresh
-                        logger.warning("Checkpoint %s: optimizer state does not match the current optimizer "
-                                       "(%s: %s); params, walkers and step restored, optimizer state "
-                                       "re-initialised", path, type(e).__name__, e)
-                        opt_state = opt_init(params)
             width = float(f["mcmc_width"])
         logger.info("Restored checkpoint %s", path)
         return step, CheckpointState(params, shard, opt_state, width)

@@ -15,6 +15,8 @@ device with no host sync (the algorithm is restated in oracle/kf
 
 from __future__ import annotations
 
+import logging
+
 import torch
 
 from . import _lib
@@ -22,6 +24,8 @@ from .config import Config, LearningRate, OptimizerName
 from .loss import LossMode, make_loss_fn
 from .networks.psiformer import ParamTree, _ptr, _stream
 from .types import CheckpointState
+
+logger = logging.getLogger(__name__)
 
 
 def lr_schedule(lr: LearningRate, t: int) -> float:
@@ -110,6 +114,11 @@ def make_kfac_training_step(cfg: Config, network):
     stepped with momentum 0 and damping 1e-3 at the schedule's learning rate."""
     loss_grad_fn = make_loss_fn(network, cfg.system, LossMode.ENERGY_GRAD, curvature=True)
     net = loss_grad_fn.network
+    if str(getattr(cfg.network.orbital, "value", cfg.network.orbital)) == "sparse":
+        # kfac.py:127-133, 175-181 (oracle/kfac.py header): the lll_weight block's statistics assume
+        # kfac_jax's matcher tags the axis-1 DenseGeneral as repeated_dense_complex_no_bias
+        logger.warning("KFAC with sparse orbitals: the lll_weight curvature block follows oracle/kfac.py's "
+                       "restatement of kfac_jax, parity unpinned against the reference (kfac_jax is absent)")
 
     def init(params, key=None, data=None):
         del key, data

@@ -215,7 +215,8 @@ def test_restore_keeps_params_when_optimizer_changed(tmp_path):
     """An Adam checkpoint (opt_state/mu, nu, count) restored into a run whose optimizer state
     has other keys (KFAC: raw, weight, step): params, walkers and step come back, the optimizer
     state is re-initialised with a warning instead of the whole checkpoint being skipped
-    (log.py restore_checkpoint)."""
+    (log.py restore_checkpoint) — only when the saved key set differs from the
+    current optimizer's; a same-optimizer state of the wrong size raises."""
     from deephall_amd import config
     from deephall_amd.log import LogManager
     from deephall_amd.networks import make_network
@@ -238,6 +239,9 @@ def test_restore_keeps_params_when_optimizer_changed(tmp_path):
             KfacLike.inits += 1
             self.raw = torch.zeros(3)
 
+        def state_dict(self):
+            return {"raw": self.raw, "weight": 0.0, "step": 0}
+
         def load_state_dict(self, d):
             self.raw.copy_(torch.as_tensor(d["raw"]))
 
@@ -245,4 +249,14 @@ def test_restore_keeps_params_when_optimizer_changed(tmp_path):
     assert step == 5 and st.mcmc_width == 0.25 and st.data.shape == (6, 3, 2)
     for k in p:
         assert torch.equal(st.params[k], p[k])
-    assert isinstance(st.opt_state, KfacLike) and KfacLike.inits == 2
+    assert isinstance(st.opt_state, KfacLike) and KfacLike.inits == 1  # the fresh state, never loaded
+    # the SAME optimizer's state with a wrong size is an error, not a silent reset
+    bad = dict(arrays)
+    for k in ("opt_state/mu", "opt_state/nu", "opt_state/count"):
+        bad.pop(k)
+    bad.update({"opt_state/raw": np.zeros(5, np.float32), "opt_state/weight": np.asarray(1.0),
+                "opt_state/step": np.asarray(1)})
+    path2 = tmp_path / "ckpt_000005.npz"
+    np.savez_compressed(path2, **bad)
+    with pytest.raises(RuntimeError):
+        LogManager.restore_checkpoint(path2, model, torch.device("cpu"), lambda params: KfacLike())

@@ -11,6 +11,8 @@ OBJ=build/ab/$NAME.$FILE.o
 EXTRA=""; [ "$FILE" = "gemm_x6.hip" ] && EXTRA="-fno-slp-vectorize"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I include $EXTRA $FLAGS \
   -c deephall_amd/csrc/$FILE -o $OBJ
-OBJS=$(ls build/gfx950/*.o | grep -v "/$FILE.o")
+# the objects of the current link (build/gfx950/link.manifest), not a glob that would pick up
+# stale objects of deleted sources
+OBJS=$(grep -v "^$FILE.o$" build/gfx950/link.manifest | sed 's#^#build/gfx950/#')
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$NAME.so $OBJS $OBJ
 echo "built ab/$NAME.so ($FLAGS)"
