@@ -47,6 +47,9 @@
 #ifndef CHAIN_TANH_EXP  // A/B knob: the chain kernel's tanh as 1 - 2 / (exp(2x) + 1) (2 transcendentals + 3 VALU)
 #define CHAIN_TANH_EXP 0
 #endif
+#ifndef CHAIN_LN1P  // A/B knob: the chain kernel's LayerNorms in one statistics round (fast variance)
+#define CHAIN_LN1P 1
+#endif
 #ifndef CHAIN_STAMP  // diagnostic builds only (tools/chain_stamp.py): per-tile phase stamps of chain_x6s
 #define CHAIN_STAMP 0
 #endif
@@ -2351,6 +2354,49 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   // two-pass mean / centred variance (eps 1e-5); the 8 wave partials of a row meet in LDS
   float x[RB][16];
   auto layernorm = [&](const float* ln) __attribute__((always_inline)) {
+#if CHAIN_LN1P
+    // ONE statistics round: sum x and sum x^2 together (flax's fast variance, the reference's
+    // own arithmetic: var = max(E[x^2] - E[x]^2, 0), oracle/reference.py:134-137), one barrier
+    // and one LDS exchange per LayerNorm instead of the two of the centred two-pass form
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f, q = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        t += (x[rb][4 * g] + x[rb][4 * g + 1]) + (x[rb][4 * g + 2] + x[rb][4 * g + 3]);
+        q += (x[rb][4 * g] * x[rb][4 * g] + x[rb][4 * g + 1] * x[rb][4 * g + 1]) +
+             (x[rb][4 * g + 2] * x[rb][4 * g + 2] + x[rb][4 * g + 3] * x[rb][4 * g + 3]);
+      }
+      t += __shfl_xor(t, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lh == 0) {
+        part[wid * CH_BM + 32 * rb + l32] = t;
+        part[(CS_NW + wid) * CH_BM + 32 * rb + l32] = q;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < CS_NW; ++w) {
+        t += part[w * CH_BM + 32 * rb + l32];
+        q += part[(CS_NW + w) * CH_BM + 32 * rb + l32];
+      }
+      const float mean = t * (1.f / 256.f);
+      const float var = fmaxf(q * (1.f / 256.f) - mean * mean, 0.f);
+      const float rs = __builtin_amdgcn_rsqf(var + 1e-5f);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gm = *reinterpret_cast<const float4*>(ln + colof(g));
+        const float4 bt = *reinterpret_cast<const float4*>(ln + CH_BN + colof(g));
+        x[rb][4 * g] = gm.x * (rs * (x[rb][4 * g] - mean)) + bt.x;
+        x[rb][4 * g + 1] = gm.y * (rs * (x[rb][4 * g + 1] - mean)) + bt.y;
+        x[rb][4 * g + 2] = gm.z * (rs * (x[rb][4 * g + 2] - mean)) + bt.z;
+        x[rb][4 * g + 3] = gm.w * (rs * (x[rb][4 * g + 3] - mean)) + bt.w;
+      }
+    }
+#else
     float s[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
@@ -2393,6 +2439,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         x[rb][4 * g + 3] = gm.w * (rs * x[rb][4 * g + 3]) + bt.w;
       }
     }
+#endif
   };
 
   // ---- P1 prologue: o rows -> planes (each element split once)
