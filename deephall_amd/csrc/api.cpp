@@ -721,7 +721,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       }
       launch_chain_x6(w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
                       last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
-                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, feat, s);
+                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, feat, s,
+                      /*store_h=*/!last);  // the last layer's h is dead: only its orbitals are read
       continue;
     }
     if (ln_fused) {
@@ -781,8 +782,9 @@ int ensure_expo(dh_handle* h) {
 }
 
 // log psi of nw walkers into logpsi [nw][2]: the Psiformer pass or the Laughlin kernel
+// epi (Psiformer only): the MCMC accept / next proposal fused into the value kernel
 int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logpsi, hipStream_t s,
-               bool geo_ready = false) {
+               bool geo_ready = false, const McmcEpi& epi = McmcEpi{}) {
   if (h->laughlin) {
     if (int rc = ensure_expo(h)) return rc;
     PROF(PK_DET_VALUE, 0.0, 8.0 * nw * h->d.N);
@@ -792,9 +794,18 @@ int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logps
   if (int rc = run_trunk(h, x, nw, 1, w, s, geo_ready)) return rc;
   {
     PROF(PK_DET_VALUE, 0.0, 4.0 * nw * h->d.N * h->d.ld_orb);
-    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s);
+    launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s, epi);
   }
   return check_launch();
+}
+
+// DH_MCMC_FUSE=0 keeps the separate accept / proposal launches (A/B measurements)
+bool mcmc_fuse_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_MCMC_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 int check_common(dh_handle* h, const void* x, int B, void* ws, size_t ws_bytes, size_t need) {
@@ -834,10 +845,13 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
   // step st: accept of st - 1 and the proposal of st in one launch (which also writes the
   // proposal's geometry, so the trunk skips its input kernel); the last accept alone
   const bool geo = !h->laughlin;
+  // Psiformer: step st's accept and step st + 1's proposal run in the epilogue of step st's
+  // value kernel (McmcEpi, det.hip): one launch fewer per move, bit-identical results
+  const bool fuse = geo && mcmc_fuse_enabled();
   for (int st = 0; st < steps; ++st) {
     const float* nz = noise ? noise + st * nstride : nullptr;
     const uint64_t step = counter + (uint64_t)st;
-    {
+    if (!fuse || st == 0) {
       PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
       if (st == 0)
         launch_propose(d, x, w.x2, B, width, seed, step, walker_offset, nz, 0, s, geo ? w.geo : nullptr);
@@ -845,9 +859,25 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
         launch_accept_propose(d, x, w.x2, geo ? w.geo : nullptr, lp, w.logpsi, n_accept, B, width, seed, step - 1,
                               walker_offset, noise ? noise + (st - 1) * nstride : nullptr, nz, s);
     }
-    if (int rc = value_pass(h, w.x2, B, w, w.logpsi, s, geo)) return rc;
+    McmcEpi epi{};
+    if (fuse) {
+      epi.on = 1;
+      epi.propose = st + 1 < steps;
+      epi.x = x;
+      epi.x2 = w.x2;
+      epi.geo = w.geo;
+      epi.lp = lp;
+      epi.nacc = n_accept;
+      epi.width = width;
+      epi.seed = seed;
+      epi.step = step;
+      epi.woff = walker_offset;
+      epi.noise = nz;
+      epi.noise2 = (noise && st + 1 < steps) ? noise + (st + 1) * nstride : nullptr;
+    }
+    if (int rc = value_pass(h, w.x2, B, w, w.logpsi, s, geo, epi)) return rc;
   }
-  if (steps > 0) {
+  if (steps > 0 && !fuse) {
     PROF(PK_MCMC, 0.0, 16.0 * B * d.N);
     launch_accept(d, x, w.x2, lp, w.logpsi, n_accept, B, seed, counter + (uint64_t)(steps - 1), walker_offset,
                   noise ? noise + (steps - 1) * nstride : nullptr, 0, s);

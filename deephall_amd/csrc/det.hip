@@ -20,6 +20,7 @@
 
 #include "dh_internal.h"
 #include "device_common.h"
+#include "mcmc_common.h"
 
 namespace dh {
 namespace {
@@ -213,7 +214,7 @@ __device__ inline double jastrow_pair(double r, double al, double cst, double* f
 template <int MGV, bool HW = false>
 __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
                                  const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
-                                 int N, int n_up, int M, int K, int nw, int per) {
+                                 int N, int n_up, int M, int K, int nw, int per, McmcEpi epi) {
   static_assert(!HW || MGV == 0, "half-wave form: serial contraction only");
   extern __shared__ float sm_all[];
   const int half = HW ? (int)(threadIdx.x >> 5) : 0;
@@ -311,6 +312,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
     if (tid == 0) ld[k] = *logdet;
     __syncthreads();
   }
+  float* lpv = reinterpret_cast<float*>(cart + 3 * N);  // this walker's Re log psi for the epilogue
   if (tid == 0 && live) {
     // log-sum-exp over determinants (psiformer.py:74-76)
     float lmax = -INFINITY;
@@ -325,7 +327,29 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
     float val_im = atan2f(zi, zr);
     logpsi[2 * b] = val_re + (float)Jw;
     logpsi[2 * b + 1] = val_im;
+    *lpv = val_re + (float)Jw;
   }
+  if (!epi.on) return;
+  // ---- MCMC epilogue (McmcEpi): the accept of epi.step for this walker and its next proposal,
+  // lane i < N moving electron i — accept_propose_kernel's arithmetic on the same values
+  __syncthreads();
+  if (!live || tid >= N) return;
+  const float lp2 = 2.f * *lpv;
+  const bool cond = accept_one(lp2, epi.lp[b], b, N, epi.seed, epi.step, epi.woff, epi.noise);
+  const int e = b * N + tid;
+  float th = epi.x[2 * e], ph = epi.x[2 * e + 1];
+  if (cond) {
+    th = x[2 * e];  // x is the proposal this kernel evaluated (epi.x2)
+    ph = x[2 * e + 1];
+    epi.x[2 * e] = th;
+    epi.x[2 * e + 1] = ph;
+    if (tid == 0) {
+      epi.lp[b] = lp2;
+      epi.nacc[b] += 1;
+    }
+  }
+  if (epi.propose)
+    propose_one(th, ph, epi.x2, epi.geo, e, b, tid, N, epi.width, epi.seed, epi.step + 1, epi.woff, epi.noise2);
 }
 
 // ------------------------------------------------------------------ envelope contraction
@@ -1736,17 +1760,18 @@ static bool det_value_hw() {
 }
 
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
-                      float* logpsi, int nw, hipStream_t s) {
-  const int per = (2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2 + 3) & ~3;  // floats
+                      float* logpsi, int nw, hipStream_t s, const McmcEpi& epi) {
+  // floats per walker region (+1: the epilogue's log psi slot after the f64 unit vectors)
+  const int per = (2 * d.N * d.M + 2 * d.N * d.N + 2 * d.N + 2 * d.K + 2 + 4 + 6 * d.N + 2 + 3 + 1) & ~3;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(nw), dim3(64), (size_t)per * sizeof(float), s, F, d.ld_orb, x, jastrow, norm,
-                       logpsi, d.N, d.n_up, d.M, d.K, nw, per);
+                       logpsi, d.N, d.n_up, d.M, d.K, nw, per, epi);
   };
   const int mgv = (d.M + 64 / d.N - 1) / (64 / d.N);  // harmonics per lane
   if (mgv <= 2 && d.N * d.N <= 64 && det_value_hw()) {
     // two walkers per wave (C2, M = 16, N = 6)
     hipLaunchKernelGGL((det_value_kernel<0, true>), dim3((nw + 1) / 2), dim3(64), (size_t)2 * per * sizeof(float), s, F,
-                       d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per);
+                       d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per, epi);
   } else if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
     go(det_value_kernel<0>);
   else if (mgv <= 4)

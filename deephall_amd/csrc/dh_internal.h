@@ -138,7 +138,8 @@ void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, cons
 // residual when feat.W0), h = LN2(h1 + tanh(h1 Wm + b2)), then Y3 = h W3 + b3 if Wp3.
 void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
-                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s);
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s,
+                     bool store_h = true);
 // dst[c][r] = src[r][c] for r < rows, c < cols (row strides ld_src / ld_dst).
 void launch_transpose(const float* src, int ld_src, int rows, int cols, float* dst, int ld_dst, hipStream_t s);
 
@@ -182,8 +183,25 @@ void launch_layernorm(const Dims& d, const float* X, const float* Z, const float
 // det.hip
 //   value mode (C == 1): logpsi[nw][2]
 //   energy mode (C == 2N+5): e_l[nw][2], obs[nw][8]
+// MCMC epilogue of the value kernel (round 5): after log psi of the proposal x2 (= the x the
+// kernel evaluates), the accept of `step` (mcmc.py:55-62: x, lp, nacc updated) and, when
+// `propose`, the next proposal of step + 1 into x2 / geo (mcmc.py:67-102) — what
+// launch_accept_propose / launch_accept do, per walker, bit for bit, without their launch.
+struct McmcEpi {
+  int on = 0, propose = 0;
+  float* x = nullptr;
+  float* x2 = nullptr;
+  float* geo = nullptr;
+  float* lp = nullptr;
+  int32_t* nacc = nullptr;
+  float width = 0.f;
+  uint64_t seed = 0, step = 0;
+  int64_t woff = 0;
+  const float* noise = nullptr;   // this step's injected noise (accept uniform)
+  const float* noise2 = nullptr;  // the next step's (its proposal)
+};
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
-                      float* logpsi, int nw, hipStream_t s);
+                      float* logpsi, int nw, hipStream_t s, const McmcEpi& epi = McmcEpi{});
 // phic != nullptr (det_precontract(d)): the channel matrices are first contracted from F by
 // env_contract_kernel into phic [nw][K][C][N][N] complex, then assembled from there
 // NetObs estimators (netobs.hip): theta / pair-angle histograms, LLL monopole harmonics

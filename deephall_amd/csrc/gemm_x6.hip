@@ -1943,6 +1943,7 @@ struct ChainArgs {
   float* h;  // residual of P1 (unless feat.W0), output of P2
   int rows;
   X6Feat feat;
+  int store_h;  // 0: P2's h is not written back (the last layer: only P3's orbitals are consumed)
 };
 
 __global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
@@ -2167,7 +2168,7 @@ __global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
                         r.z + tanh_rat(acc[j][4 * g + 2] + bv.z), r.w + tanh_rat(acc[j][4 * g + 3] + bv.w));
     }
   __syncthreads();
-  ln_rows(nullptr, a.ln2, nullptr, false, a.h);
+  ln_rows(nullptr, a.ln2, nullptr, false, a.store_h ? a.h : nullptr);
   if (!a.Wp3) return;
   __syncthreads();
   // ---- P3: Y3 = h2 W3 + b3, 256-column tiles, stored from the MFMA layout (16-B pieces)
@@ -2591,7 +2592,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     for (int g = 0; g < 4; ++g) {
       const float4 y = make_float4(x[rb][4 * g], x[rb][4 * g + 1], x[rb][4 * g + 2], x[rb][4 * g + 3]);
       if (a.Wp3) put4(32 * rb + l32, colof(g), y);
-      if (r < rows) *reinterpret_cast<float4*>(a.h + (size_t)r * CH_BN + colof(g)) = y;
+      if (a.store_h && r < rows) *reinterpret_cast<float4*>(a.h + (size_t)r * CH_BN + colof(g)) = y;
     }
   }
   if (!a.Wp3) return;
@@ -3239,8 +3240,9 @@ bool chain_x6_enabled() {
 // rows; Wp3 may be null (no P3); Y3 rows 16-B aligned (ldy3 % 4 == 0).
 void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
-                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s) {
-  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, feat};
+                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s,
+                     bool store_h) {
+  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, feat, store_h ? 1 : 0};
   static const int form = [] {  // DH_CHAIN=2: the LDS-ring form; 3, 4: ablations (tools only)
     const char* e = std::getenv("DH_CHAIN");
     return e ? e[0] - '0' : 1;
@@ -3297,7 +3299,7 @@ void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, cons
   X6Feat f{};
   f.geo = geo;
   f.N = N;
-  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, f};
+  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, f, 1};
   auto go = [&](auto kern, int C) {
     const int RV = (CH_BM / C) * C;
     ensure_smem(kern, CS_SMEM);
