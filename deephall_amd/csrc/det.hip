@@ -637,6 +637,183 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ envelope contraction, streamed
+// Round 5 form of env_contract_kernel for long rows (C5: 2 M N = 2320 floats per channel row):
+// the same sums, but the rows come straight into registers by plain loads, D rows ahead (the
+// compiler counts them: no LDS ring, no hand-counted vmcnt), so a wave keeps D - 1 rows
+// (~17 KB at C5) in flight instead of the ring's three — the ring form read F at ~3 TB/s,
+// bounded by the bytes in flight per CU, not by HBM.  One 256-thread workgroup per (walker,
+// electron), four waves over contiguous harmonic blocks (MW = ceil(M / 4) each), lane (j, g)
+// on harmonics MW w + g + G u (u < MG); the channel loop is unrolled (C compile-time) so the
+// register ring is indexed by constants.  The leaves, the per-row sums, the lane-group and
+// cross-wave reductions and the PhiC layout are env_contract_kernel's (K = 1).
+template <int N, int MG, int D>
+__global__ __launch_bounds__(256, 2) void env_stream_kernel(const float* __restrict__ Fp, int ldF,
+                                                            const float* __restrict__ x,
+                                                            const float* __restrict__ geo_g,
+                                                            const float* __restrict__ norm, float* __restrict__ PhiC,
+                                                            int n_up, int M) {
+  constexpr int T = 2 * N, C = 2 * N + 5, G = 64 / N, NK = N;
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x / N, i = blockIdx.x - (blockIdx.x / N) * N;
+  cf* wt = reinterpret_cast<cf*>(sm);                  // [E0, DTH, DPH, LB, W0..2, SF0..2][M + 1]
+  cf* part = wt + 10 * (M + 1);                        // [4 waves][C][N]
+  cf* sink = part + 4 * C * N;                         // [4 waves][64]: lanes g > 0 store here
+  float* al = reinterpret_cast<float*>(sink + 256);    // [3][T]
+  const int j = lane % N, g = lane / N;
+  const int MW = (M + 3) / 4, gg = MW * wv + g, mend = min(MW * (wv + 1), M), M1 = M + 1;
+  const bool act = g < G;
+  const int blk = (i >= n_up && n_up > 0) ? 1 : 0, MNK = M * NK;
+  // uniform row base (scalar address) + 32-bit lane offsets: one voffset per harmonic
+  const float* rowbase = Fp + ((size_t)(b * N + i) * C) * ldF + (size_t)blk * 2 * MNK;
+  // lane harmonic u: m = gg + G u (clamped for the address; masked in the sums)
+  // masked lanes read harmonic M - 1 and multiply it by the zero factor at index M
+  int mo[MG], mw_[MG];
+#pragma unroll
+  for (int u = 0; u < MG; ++u) {
+    const bool ok = act && gg + G * u < mend;
+    mo[u] = min(gg + G * u, M - 1) * NK + j;
+    mw_[u] = ok ? gg + G * u : M;
+  }
+  // buffer loads: scalar resource + row soffset, 32-bit lane voffsets (no 64-bit lane addresses)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rowbase), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < MG; ++u) mo[u] *= 4;
+  float fr[D][MG][2];
+  auto load_row = [&](int c, float (&f)[MG][2]) __attribute__((always_inline)) {
+    const int so = c * ldF * 4;
+#pragma unroll
+    for (int u = 0; u < MG; ++u) {
+      f[u][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, mo[u], so, 0));
+      f[u][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, mo[u] + MNK * 4, so, 0));
+    }
+  };
+  // the value row and the first D - 1 tangent rows are requested before the leaves are computed
+  float f0[MG][2];
+  load_row(0, f0);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) load_row(1 + d, fr[d]);
+  {
+    const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + i));
+    const float th = x[2 * (b * N + i)], ph = x[2 * (b * N + i) + 1];
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const float gauge = env_gauge(ct, M);
+    const float phh[3] = {-sp, cp, 0.f};
+    const float thh[3] = {ct * cp, ct * sp, -st};
+    if (tid < 10) wt[tid * M1 + M] = cf{0.f, 0.f};
+    for (int p = tid; p < M; p += 256) {
+      const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge);
+      wt[p] = e.e0;
+      wt[M1 + p] = e.dth;
+      wt[2 * M1 + p] = e.dph;
+      wt[3 * M1 + p] = e.lb;
+      const float mf = (float)p - 0.5f * (float)(M - 1) - gauge;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        wt[(4 + k) * M1 + p] = cf{phh[k] * e.dth.re - thh[k] * e.dph.re, phh[k] * e.dth.im - thh[k] * e.dph.im};
+        wt[(7 + k) * M1 + p] = env_flow2(e.e0, e.dth, e.d2th, mf, st, ct, sp, cp, k);
+      }
+    }
+    if (tid < T) {  // alpha_kt from the geometry of the electron tangent t moves
+      const float4 ga = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + (tid >> 1)));
+      al[tid] = (tid & 1) ? -(ga.y * ga.w) : -ga.z;
+      al[T + tid] = (tid & 1) ? -(ga.y * ga.z) : ga.w;
+      al[2 * T + tid] = (tid & 1) ? ga.x : 0.f;
+    }
+  }
+  __syncthreads();
+  // the envelope factors are re-read from LDS per row (the index is laundered so that they are
+  // not hoisted into registers: the VGPRs go to rows in flight instead)
+  // per-row result store without a branch (a branch per row splits the unrolled bodies into
+  // blocks and lets the compiler sink the row sums past them, keeping every row live)
+  cf* const dst = g == 0 ? part + (size_t)wv * C * N + j : sink + tid;
+  const int dstride = g == 0 ? N : 0;
+  auto gsum = [&](float v) __attribute__((always_inline)) {
+    float r = v;
+#pragma unroll
+    for (int q = 1; q < G; ++q) r += __shfl(v, j + N * q, 64);
+    return r;
+  };
+  cf xd{0.f, 0.f}, xp{0.f, 0.f}, xl{0.f, 0.f}, xs0{0.f, 0.f}, xs1{0.f, 0.f}, xs2{0.f, 0.f};  // F_0 extras
+  cf lb2{0.f, 0.f}, gu0{0.f, 0.f}, gu1{0.f, 0.f}, gu2{0.f, 0.f};                            // lane partials
+  {  // value row (c = 0)
+    cf e0a{0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < MG; ++u) {
+      const cf fv{f0[u][0], f0[u][1]};
+      const int m = mw_[u];
+      cfma(e0a, fv, wt[m]);
+      cfma(xd, fv, wt[M1 + m]);
+      cfma(xp, fv, wt[2 * M1 + m]);
+      cfma(xl, fv, wt[3 * M1 + m]);
+      cfma(xs0, fv, wt[7 * M1 + m]);
+      cfma(xs1, fv, wt[8 * M1 + m]);
+      cfma(xs2, fv, wt[9 * M1 + m]);
+    }
+    const cf v{gsum(e0a.re), gsum(e0a.im)};
+    dst[0] = v;
+  }
+  // tangent rows c = 1..T: branch-free bodies (own-electron terms weighted by 0/1), loads for
+  // row min(c + D - 1, C - 1) issued unconditionally, so the loop is straight-line and the
+  // compiler's vmcnt keeps D - 1 rows in flight
+  static_assert(T % D == 0, "tangent rows come in whole groups of D");
+#pragma nounroll
+  for (int c0 = 1; c0 <= T; c0 += D) {
+#pragma unroll
+    for (int dd_ = 0; dd_ < D; ++dd_) {
+      const int c = c0 + dd_, t = c - 1;
+      __builtin_amdgcn_sched_barrier(0);  // keep the ring order: one row's loads per body
+      load_row(min(c + D - 1, C - 1), fr[(dd_ + D - 1) % D]);
+      const float (&f)[MG][2] = fr[dd_];
+      const float ownf = (t >> 1) == i ? 1.f : 0.f;
+      const int dsel = (t & 1) ? 2 * M1 : M1;
+      cf e0a{0.f, 0.f}, w0{0.f, 0.f}, w1{0.f, 0.f}, w2{0.f, 0.f}, dd{0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < MG; ++u) {
+        const cf fv{f[u][0], f[u][1]};
+        int m = mw_[u];
+        asm volatile("" : "+v"(m));
+        cfma(e0a, fv, wt[m]);
+        cfma(w0, fv, wt[4 * M1 + m]);
+        cfma(w1, fv, wt[5 * M1 + m]);
+        cfma(w2, fv, wt[6 * M1 + m]);
+        cfma(dd, fv, wt[dsel + m]);
+      }
+      lb2 += ownf * dd;
+      e0a += ownf * ((t & 1) ? xp : xd);
+      gu0 += al[t] * w0;
+      gu1 += al[T + t] * w1;
+      gu2 += al[2 * T + t] * w2;
+      const cf v{gsum(e0a.re), gsum(e0a.im)};
+      dst[c * dstride] = v;
+    }
+  }
+  // rows T + 1..T + 4 (L, S_0..2) are in ring slots 0..3
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = T + 1 + r;
+    const float (&f)[MG][2] = fr[r];
+    cf e0a{0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < MG; ++u) cfma(e0a, cf{f[u][0], f[u][1]}, wt[mw_[u]]);
+    if (r == 0) e0a += xl + 2.f * lb2;
+    if (r == 1) e0a += xs0 + 2.f * gu0;
+    if (r == 2) e0a += xs1 + 2.f * gu1;
+    if (r == 3) e0a += xs2 + 2.f * gu2;
+    const cf v{gsum(e0a.re), gsum(e0a.im)};
+    dst[c * dstride] = v;
+  }
+  __syncthreads();
+  float* out = PhiC + 2 * ((size_t)b * C * N * N + (size_t)i * N);
+  for (int e = tid; e < C * N; e += 256) {
+    const int c = e / N, jj = e - (e / N) * N;
+    const cf v = (part[e] + part[C * N + e]) + (part[2 * C * N + e] + part[3 * C * N + e]);
+    out[2 * ((size_t)c * N * N + jj)] = v.re;
+    out[2 * ((size_t)c * N * N + jj) + 1] = v.im;
+  }
+}
+
 // dynamic LDS of env_contract_kernel<MG, WU>
 size_t env_contract_smem(int N, int M, int MG, bool WU, int K = 1, bool seg = false) {
   const int T = 2 * N, C = 2 * N + 5;
@@ -1899,6 +2076,22 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
       hipLaunchKernelGGL(kern, dim3(grid), dim3(256), eb, s, F, d.ld_orb, x, geo, norm, phic, nw, d.N, d.n_up, d.M,
                          d.K, d.Q);
     };
+    // C5 (N = 20, one spin block, K = 1): rows streamed through registers (env_stream_kernel)
+    static const bool stream = [] {
+      const char* e = std::getenv("DH_ENV_STREAM");
+      return !(e && e[0] == '0');
+    }();
+    const int mgs = ((d.M + 3) / 4 + (64 / d.N) - 1) / (64 / d.N);  // harmonics per lane, four waves
+    if (stream && d.N == 20 && d.K == 1 && mgs <= 5) {
+      const size_t eb = ((size_t)10 * (d.M + 1) * 2 + 4 * (2 * d.N + 5) * d.N * 2 + 512 + 3 * 2 * d.N) * sizeof(float);
+      hipLaunchKernelGGL((env_stream_kernel<20, 5, 8>), dim3(nw * d.N), dim3(256), eb, s, F, d.ld_orb, x, geo, norm,
+                         phic, d.n_up, d.M);
+      if (one_wave)
+        go(det_energy_kernel<0, true, 64>);
+      else
+        go(det_energy_kernel<0, true>);
+      return;
+    }
     if (mgw <= 4) {  // short rows (C4: M = 24, N = 10): a wave per electron
       switch (mgw) {
         case 1: env(env_contract_kernel<1, true>, 1, true); break;
