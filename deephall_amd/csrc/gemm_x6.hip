@@ -26,6 +26,7 @@
 // once.  B planes are staged by LDS-DMA into [plane][BN][64 B] images, 16-B slots
 // swizzled by (row>>2)&3 (16 lanes of a ds_read_b128 pass hit 16 distinct bank groups).
 #include <cstdlib>
+#include <type_traits>
 
 #include "attn_val.h"
 #include "dh_internal.h"
@@ -50,6 +51,9 @@
 #ifndef CHAIN_LN1P  // A/B knob: the chain kernel's LayerNorms in one statistics round (fast variance)
 #define CHAIN_LN1P 1
 #endif
+#ifndef CHAIN_P3T  // A/B knob: P3 MFMAs with the operands swapped (accumulator = tile row x 32 columns,
+#define CHAIN_P3T 1  // one register = two 128-B row segments: full-rate dword stores) instead of float4
+#endif               // stores of 32 rows x 32 B per instruction (round 5)
 #ifndef CHAIN_STAMP  // diagnostic builds only (tools/chain_stamp.py): per-tile phase stamps of chain_x6s
 #define CHAIN_STAMP 0
 #endif
@@ -2299,7 +2303,15 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
   };
-  auto gemm = [&]() __attribute__((always_inline)) {
+  // TR: the operands swapped, D[tile row][output column] (P3's store layout, CHAIN_P3T)
+  auto gemm = [&](auto tr_) __attribute__((always_inline)) {
+    constexpr bool TR = decltype(tr_)::value;
+    auto mf = [](const bf16x8& w, const bf16x8& x, const f32x16& c) __attribute__((always_inline)) {
+      if constexpr (TR)
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w, c, 0, 0, 0);
+      else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, x, c, 0, 0, 0);
+    };
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2329,17 +2341,17 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       // product-major over the three row blocks: consecutive MFMAs are independent
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][2], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b0, ca[rb][2], acc[rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, ca[rb][0], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b2, ca[rb][0], acc[rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][1], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b1, ca[rb][1], acc[rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][1], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b0, ca[rb][1], acc[rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][0], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b1, ca[rb][0], acc[rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][0], acc[rb], 0, 0, 0);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = mf(b0, ca[rb][0], acc[rb]);
       __builtin_amdgcn_sched_barrier(0);
       if (kt + 1 < nk) {
 #pragma unroll
@@ -2349,6 +2361,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       }
     }
   };
+  using NoTr = std::integral_constant<bool, false>;
   // MFMA layout: reg 4 g + e of acc[rb] = tile row 32 rb + l32, column 32 wid + 8 g + 4 lh + e
   auto colof = [&](int g) __attribute__((always_inline)) { return 32 * wid + 8 * g + 4 * lh; };
   // LayerNorm of the values x (MFMA layout, 16 per lane and row block) in registers:
@@ -2511,7 +2524,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
   // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
   CHAIN_T(1);
-  gemm();
+  gemm(NoTr{});
   CHAIN_T(2);
   prefetch(a.Wp2, a.ldp2, 0);
   {
@@ -2563,7 +2576,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   __syncthreads();
   // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
   CHAIN_T(5);
-  gemm();
+  gemm(NoTr{});
   CHAIN_T(6);
   if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
 #pragma unroll
@@ -2601,8 +2614,31 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
   for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
     if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
-    gemm();
+    gemm(std::integral_constant<bool, CHAIN_P3T != 0>{});
     if (col0 < 3 * CH_BN) CHAIN_T(10 + 2 * (col0 / CH_BN));
+#if CHAIN_P3T
+    {  // D[tile row][column]: reg q of acc[rb] = row 32 rb + (q & 3) + 8 (q >> 2) + 4 lh, column l32.
+      // Buffer stores: the tile's rows as the resource (rows past the batch fall outside it and
+      // are dropped), the row offset as soffset, one 32-bit lane offset (past the range off n3)
+      const int c = col0 + 32 * wid + l32;
+      const bool cok = c < a.n3;
+      const float bv = cok ? a.b3[c] : 0.f;
+      if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
+      const int nrow = min(CH_BM, rows - row0), ldb = a.ldy3 * 4;
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.Y3 + (size_t)row0 * a.ldy3, (short)0, nrow * ldb, 0x00020000);
+      const int vo = cok ? 4 * lh * ldb + 4 * c : 0x7fffffff;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        if (ABLS == 2 && acc[rb][0] != 1234.5f) continue;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[rb][q] + bv), rs, vo,
+                                                (32 * rb + (q & 3) + 8 * (q >> 2)) * ldb, 0);
+      }
+      if (col0 < 3 * CH_BN) CHAIN_T(11 + 2 * (col0 / CH_BN));
+      continue;
+    }
+#endif
     // this lane's 16 bias values first (one wait), THEN the prefetch and the stores: a bias load
     // between two stores waits for every earlier store (vmcnt counts in order)
     float4 b3v[4];

@@ -131,12 +131,15 @@ def audit(path: Path):
                     if plab:
                         younger.append("<label>")
                         continue
+                    if p.startswith("s_cbranch") or p.startswith("s_branch"):
+                        younger.append("<" + p.split()[0] + ">")
+                        continue
                     if (pasm and p.startswith("s_waitcnt") and "vmcnt" in p) or p.startswith("s_barrier"):
                         if len([y for y in younger if y not in ("<label>",)]) >= n or p.startswith("s_waitcnt"):
                             break
                     if VMEM.match(p):
                         younger.append(("DMA" if (pasm and "lds" in p) else p.split()[0]))
-                    if len([y for y in younger if y != "<label>"]) > n + 8:
+                    if len([y for y in younger if not y.startswith("<")]) > n + 8:
                         break
                 waits.append((n, younger[:n + 8]))
         rows.append((name, meta, ndma, h1, h2, waits))
@@ -160,9 +163,24 @@ def main():
                 bad += 1
                 print(f"    H2 HAZARD: m0 write directly before {ins!r}")
             for n, y in waits:
-                dma_first = y[:n]
-                ok = all(t == "DMA" for t in dma_first if t != "<label>") and len([t for t in dma_first if t != "<label>"]) >= n
-                tag = "ok " if ok else "CHECK"
+                # the walk back to the n-th youngest VMEM op: straight-line when no branch lies on it
+                ops, walked = 0, []
+                for t in y:
+                    walked.append(t)
+                    if not t.startswith("<"):
+                        ops += 1
+                        if ops >= n:
+                            break
+                branches = [t for t in walked if t.startswith("<s_")]
+                nondma = [t for t in walked if not t.startswith("<") and t != "DMA"]
+                if ops < n:
+                    tag = "CHECK(short)"
+                elif branches:
+                    tag = "CHECK(branch)"
+                elif nondma:
+                    tag = "ok(+loads)"
+                else:
+                    tag = "ok "
                 print(f"    vmcnt({n}) {tag} youngest-first: {' '.join(t if isinstance(t, str) else t for t in y)}")
     print(f"hazards: {bad}")
 
