@@ -1353,6 +1353,331 @@ __global__ __launch_bounds__(64) void attention_feat_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// attention_feat_kernel restructured (round 5, "feat2"): the same rules in the same feature
+// space, with the tangent channels in O(N) per channel instead of O(N^2) LDS passes and O(N^3)
+// row sums.  S_t lives on row e and column e only (Srow_j = s f~e^T M f~0_j, Scol_i = s f~0_i^T
+// M f~e), so
+//   m1_i = <S_t>_A0,i = A0_ie Scol_i (i != e),  sum_j A0_ej S_t,ej (i = e);
+//   o^_t,i = sum_j A_t,ij f~0_j + A0_ie f~e = m1_i (f~0_e - o^_0,i) + A0_ie f~e  (i != e; o^_0 = A0 f~0),
+//   row e directly (N terms);  oL += 2 A_t,ie f~e.
+// The dense accumulators T2 = sum_t Sbar_t^2 and SuB_k = sum_t alpha_kt Sbar_t stay in registers
+// on the pairs each lane owns (p = lane + 64 u), and Au_k = sum_t alpha_kt A_t = A0 * SuB_k is
+// formed once for the flow channels.  The four dense channels (L, S_0..2) keep the pairwise
+// form.  LDS: A0 and three N x N scratch arrays, the rest small (C5: 10 KB per wave).
+template <int N>
+struct Feat2Smem {
+  static constexpr int nn = N * N, T = 2 * N;
+  static constexpr int G = 0, F0 = G + 4 * N, OH0 = F0 + 5 * N, GK = OH0 + 5 * N, AL = GK + 15 * N, ACC = AL + 3 * T,
+                       SR = ACC + N, SC = SR + N, M1 = SC + N, M2 = M1 + N, OH = M2 + N, FC = OH + 5 * N,
+                       A0 = FC + 5 * N, S = A0 + nn, P = S + nn, RM = P + nn, TOTAL = RM + nn;
+};
+
+template <int N>
+__global__ __launch_bounds__(64) void attention_feat2_kernel(const float* __restrict__ geo, float* __restrict__ o,
+                                                             int H, const float* __restrict__ W0qkv,
+                                                             const float* __restrict__ bqkv,
+                                                             const float* __restrict__ Mqk, int n_up) {
+  constexpr int dh = 64, T = 2 * N, C = 2 * N + 5, nn = N * N;
+  constexpr int PP = (nn + 63) / 64, QQ = (5 * N + 63) / 64;  // pairs / (electron, component) per lane
+  using L = Feat2Smem<N>;
+  extern __shared__ float sm[];
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H, lane = threadIdx.x;
+  const int D = H * dh;
+  auto wsync = [] { __builtin_amdgcn_wave_barrier(); };
+  float *g = sm + L::G, *f0 = sm + L::F0, *oh0 = sm + L::OH0, *gk = sm + L::GK, *al = sm + L::AL, *accS = sm + L::ACC;
+  float *SR = sm + L::SR, *SC = sm + L::SC, *M1 = sm + L::M1, *M2 = sm + L::M2, *oh = sm + L::OH, *fc = sm + L::FC;
+  float *A0 = sm + L::A0, *Ss = sm + L::S, *Ps = sm + L::P, *Rm = sm + L::RM;
+  const int col = h * dh + lane;
+  const float4 wv = make_float4(W0qkv[2 * D + col], W0qkv[3 * D + 2 * D + col], W0qkv[6 * D + 2 * D + col],
+                                W0qkv[9 * D + 2 * D + col]);
+  const float bv = bqkv[2 * D + col];
+  float Mr[25];
+#pragma unroll
+  for (int q = 0; q < 25; ++q) Mr[q] = Mqk[h * kMqkStride + q];
+  for (int i = lane; i < N; i += 64) {
+    const float4 gi = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
+    g[4 * i] = gi.x;
+    g[4 * i + 1] = gi.y;
+    g[4 * i + 2] = gi.z;
+    g[4 * i + 3] = gi.w;
+    const float4 f = feature_channel<T>(0, i, gi, (i < n_up) ? 1.f : -1.f);
+    f0[5 * i] = f.x;
+    f0[5 * i + 1] = f.y;
+    f0[5 * i + 2] = f.z;
+    f0[5 * i + 3] = f.w;
+    f0[5 * i + 4] = 1.f;
+    accS[i] = 0.f;
+  }
+  for (int t = lane; t < T; t += 64) {
+    const int i = t >> 1;
+    const float4 gi = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+    const float st = gi.x, ct = gi.y, sp = gi.z, cp = gi.w;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float a;
+      if ((t & 1) == 0)
+        a = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+      else
+        a = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+      al[k * T + t] = a;
+    }
+  }
+  for (int q = lane; q < 3 * N; q += 64) {  // g_k,i: alpha-weighted tangent seeds of electron i
+    const int k = q / N, i = q - k * N;
+    const float4 gi = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+    const float st = gi.x, ct = gi.y, sp = gi.z, cp = gi.w;
+    const float ae = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
+    const float ao = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
+    float* d = gk + (k * N + i) * 5;
+    d[0] = -ae * st;
+    d[1] = ae * ct * cp - ao * sp;
+    d[2] = ae * ct * sp + ao * cp;
+    d[3] = 0.f;
+    d[4] = 0.f;
+  }
+  wsync();
+  auto form = [&](const float* x, const float* y) __attribute__((always_inline)) {
+    float sres = 0.f;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      float u = 0.f;
+#pragma unroll
+      for (int c2 = 0; c2 < 5; ++c2) u = fmaf(Mr[5 * a + c2], y[c2], u);
+      sres = fmaf(x[a], u, sres);
+    }
+    return sres;
+  };
+  float* obase = o + (size_t)b * N * C * D + col;
+  auto expand = [&](int c) __attribute__((always_inline)) {
+    wsync();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float* u = oh + 5 * i;
+      const float v = fmaf(u[0], wv.x, fmaf(u[1], wv.y, fmaf(u[2], wv.z, fmaf(u[3], wv.w, u[4] * bv))));
+      obase[(size_t)(i * C + c) * D] = v;
+    }
+  };
+
+  // ---- value channel: A0 = softmax(f~0 Mqk f~0^T), o^_0 = A0 f~0
+  float a0r[PP];
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    const int p = lane + 64 * u;
+    if (p < nn) {
+      const int i = p / N, j = p - (p / N) * N;
+      A0[p] = form(f0 + 5 * i, f0 + 5 * j);
+    }
+  }
+  wsync();
+  for (int i = lane; i < N; i += 64) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = fmaxf(m, A0[i * N + j]);
+    float e[N], ssum = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      e[j] = expf(A0[i * N + j] - m);
+      ssum += e[j];
+    }
+    const float inv = 1.f / ssum;
+#pragma unroll
+    for (int j = 0; j < N; ++j) A0[i * N + j] = e[j] * inv;
+  }
+  wsync();
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    const int p = lane + 64 * u;
+    a0r[u] = p < nn ? A0[p] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < QQ; ++u) {
+    const int q = lane + 64 * u;
+    if (q < 5 * N) {
+      const int i = q / 5, a = q - (q / 5) * 5;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fmaf(A0[i * N + j], f0[5 * j + a], acc);
+      oh0[q] = acc;
+      oh[q] = acc;
+    }
+  }
+  expand(0);
+
+  // ---- tangents
+  float T2r[PP], SuBr[3][PP], oLr[QQ];
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    T2r[u] = 0.f;
+    SuBr[0][u] = SuBr[1][u] = SuBr[2][u] = 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < QQ; ++u) oLr[u] = 0.f;
+#pragma unroll 1
+  for (int t = 0; t < T; ++t) {
+    const int c = 1 + t, e = t >> 1;
+    float fe[5];
+    {
+      const float4 ge = make_float4(g[4 * e], g[4 * e + 1], g[4 * e + 2], g[4 * e + 3]);
+      const float4 f = feature_channel<T>(c, e, ge, (e < n_up) ? 1.f : -1.f);
+      fe[0] = f.x;
+      fe[1] = f.y;
+      fe[2] = f.z;
+      fe[3] = f.w;
+      fe[4] = 0.f;
+    }
+    for (int j = lane; j < N; j += 64) {
+      SR[j] = form(fe, f0 + 5 * j);
+      SC[j] = form(f0 + 5 * j, fe);
+    }
+    if (lane == 0) accS[e] += 2.f * form(fe, fe);  // s q_t . k_t, twice (S_L)
+    wsync();
+    for (int i = lane; i < N; i += 64) {
+      float m1;
+      if (i != e) {
+        m1 = A0[i * N + e] * SC[i];
+      } else {
+        m1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) m1 = fmaf(A0[e * N + j], SR[j] + (j == e ? SC[e] : 0.f), m1);
+      }
+      M1[i] = m1;
+    }
+    wsync();
+    const float a_0 = al[t], a_1 = al[T + t], a_2 = al[2 * T + t];
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int p = lane + 64 * u;
+      if (p < nn) {
+        const int i = p / N, j = p - (p / N) * N;
+        const float sv = (i == e ? SR[j] : 0.f) + (j == e ? SC[i] : 0.f);
+        const float sb = sv - M1[i];
+        T2r[u] = fmaf(sb, sb, T2r[u]);
+        SuBr[0][u] = fmaf(a_0, sb, SuBr[0][u]);
+        SuBr[1][u] = fmaf(a_1, sb, SuBr[1][u]);
+        SuBr[2][u] = fmaf(a_2, sb, SuBr[2][u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < QQ; ++u) {
+      const int q = lane + 64 * u;
+      if (q < 5 * N) {
+        const int i = q / 5, a = q - (q / 5) * 5;
+        const float m1 = M1[i], a0ie = A0[i * N + e];
+        float acc, atie;
+        if (i != e) {
+          acc = m1 * (f0[5 * e + a] - oh0[q]);
+          atie = a0ie * (SC[i] - m1);
+        } else {
+          acc = 0.f;
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            const float at = A0[e * N + j] * ((SR[j] + (j == e ? SC[e] : 0.f)) - m1);
+            acc = fmaf(at, f0[5 * j + a], acc);
+          }
+          atie = a0ie * ((SR[e] + SC[e]) - m1);
+        }
+        acc = fmaf(a0ie, fe[a], acc);
+        oLr[u] = fmaf(2.f * atie, fe[a], oLr[u]);
+        oh[q] = acc;
+      }
+    }
+    expand(c);
+  }
+  // ---- Laplace-Beltrami and flow channels (dense seeds on every electron)
+#pragma unroll 1
+  for (int c = T + 1; c < C; ++c) {
+    const int k = c - T - 2;  // flow axis (k < 0: the Laplace-Beltrami channel)
+    wsync();
+    for (int i = lane; i < N; i += 64) {
+      const float4 gi = make_float4(g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]);
+      const float4 f = feature_channel<T>(c, i, gi, (i < n_up) ? 1.f : -1.f);
+      fc[5 * i] = f.x;
+      fc[5 * i + 1] = f.y;
+      fc[5 * i + 2] = f.z;
+      fc[5 * i + 3] = f.w;
+      fc[5 * i + 4] = 0.f;
+    }
+    wsync();
+    float sr[PP], pr[PP];
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int p = lane + 64 * u;
+      sr[u] = pr[u] = 0.f;
+      if (p < nn) {
+        const int i = p / N, j = p - (p / N) * N;
+        float sv = form(fc + 5 * i, f0 + 5 * j) + form(f0 + 5 * i, fc + 5 * j);
+        float pv;
+        if (k < 0) {
+          if (i == j) sv += accS[i];
+          pv = T2r[u];
+        } else {
+          sv += 2.f * form(gk + (k * N + i) * 5, gk + (k * N + j) * 5);
+          const float sbk = k == 0 ? SuBr[0][u] : (k == 1 ? SuBr[1][u] : SuBr[2][u]);
+          pv = sbk * sbk;
+        }
+        sr[u] = sv;
+        pr[u] = pv;
+        Ss[p] = sv;
+        Ps[p] = pv;
+      }
+    }
+    wsync();
+    for (int i = lane; i < N; i += 64) {
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        m1 = fmaf(A0[i * N + j], Ss[i * N + j], m1);
+        m2 = fmaf(A0[i * N + j], Ps[i * N + j], m2);
+      }
+      M1[i] = m1;
+      M2[i] = m2;
+    }
+    wsync();
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int p = lane + 64 * u;
+      if (p < nn) {
+        const int i = p / N;
+        Rm[p] = a0r[u] * ((sr[u] - M1[i]) + (pr[u] - M2[i]));
+        if (k >= 0) {  // Au_k = A0 * SuB_k, over the scores (read above)
+          const float sbk = k == 0 ? SuBr[0][u] : (k == 1 ? SuBr[1][u] : SuBr[2][u]);
+          Ss[p] = a0r[u] * sbk;
+        }
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int u = 0; u < QQ; ++u) {
+      const int q = lane + 64 * u;
+      if (q < 5 * N) {
+        const int i = q / 5, a = q - (q / 5) * 5;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], f0[5 * j + a], fmaf(A0[i * N + j], fc[5 * j + a], acc));
+        if (k < 0) {
+          acc += oLr[u];
+        } else {
+          float a2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < N; ++j) a2 = fmaf(Ss[i * N + j], gk[(k * N + j) * 5 + a], a2);
+          acc = fmaf(2.f, a2, acc);
+        }
+        oh[q] = acc;
+      }
+    }
+    expand(c);
+  }
+}
+
+static bool attn_feat2_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_ATTN_FEAT2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // DH_ATTN_FEAT=0 keeps attention_wave_kernel<N, true> / the MFMA kernel for layer 1's channel
 // attention (A/B measurements)
 static bool attn_feat_enabled() {
@@ -1366,6 +1691,13 @@ static bool attn_feat_enabled() {
 template <int N>
 void launch_feat(const Dims& d, const float* geo, float* o, int nw, const float* W0qkv, const float* bqkv,
                  const float* Mqk, hipStream_t s) {
+  if (attn_feat2_enabled()) {
+    const size_t smem2 = (size_t)Feat2Smem<N>::TOTAL * sizeof(float);
+    ensure_smem(attention_feat2_kernel<N>, smem2);
+    hipLaunchKernelGGL(attention_feat2_kernel<N>, dim3(nw * d.H), dim3(64), smem2, s, geo, o, d.H, W0qkv, bqkv, Mqk,
+                       d.n_up);
+    return;
+  }
   const size_t smem = (size_t)FeatAttnSmem<N>::TOTAL * sizeof(float);
   ensure_smem(attention_feat_kernel<N>, smem);
   hipLaunchKernelGGL(attention_feat_kernel<N>, dim3(nw * d.H), dim3(64), smem, s, geo, o, d.H, W0qkv, bqkv, Mqk,
