@@ -633,6 +633,14 @@ namespace {
 // One Psiformer pass over nw walkers with C channels; leaves orbital features in w.F.
 // geo_ready: w.geo already holds the walkers' geometry (written by the MCMC proposal); the
 // input kernel is then skipped when the geometry is all it would write.
+static bool lnch_feat_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DH_LNCH_FEAT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false) {
   const Dims& d = h->d;
   const Params& P = h->p;
@@ -678,11 +686,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // local energy, split-bf16, D = 256, N <= 8: GEMM + channel LayerNorm fused per map
   const bool lnch = C > 1 && x6 && !chain_ch && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&
                     gemm_lnch_supported(d.N, D);
+  // local energy, gemm_lnch: layer 1's residual h0 = f W0 is formed in the first launch's
+  // epilogue from geo (DH_LNCH_FEAT=0 keeps the input kernel writing h0)
+  const bool lnch_feat = lnch && d.L > 0 && lnch_feat_enabled();
   {
     const bool wq = fold && !fused;
     if (!(geo_ready && h_feat && !wq)) {
       PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
-      launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, h_feat ? nullptr : w.h,
+      launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, (h_feat || lnch_feat) ? nullptr : w.h,
                    wq ? w.qkv : nullptr, w.geo, nw, C, s);
     }
   }
@@ -749,7 +760,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       // (gemm_lnch.hip; the GEMM output never reaches HBM)
       {
         PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
-        launch_gemm_lnch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.geo, w.h, nw * d.N, 0, s);
+        launch_gemm_lnch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.geo, w.h, nw * d.N, 0, s,
+                         (lnch_feat && l == 0) ? P.W0 : nullptr, d.n_up);
       }
       {
         PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));

@@ -124,7 +124,8 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 bool gemm_lnch_supported(int N, int D);
 int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel; returns the previous form
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                      const float* geo, float* h, int ne, int mode, hipStream_t s);
+                      const float* geo, float* h, int ne, int mode, hipStream_t s,
+                      const float* W0f = nullptr, int n_up = 0);
 bool chain_x6_enabled();
 bool chain_attn_supported(int N, int H, int dh);
 // Channel-row (C > 1) layer tail in one launch (gemm_x6.hip chain_ch_kernel; D = 256):

@@ -141,11 +141,12 @@ __device__ __forceinline__ float lnch_sum4g(float v) {
 }
 #endif
 
-template <int N, int MODE, int NWV>
+template <int N, int MODE, int NWV, bool FRES = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >= 8 ? 2 : 1, NWV >= 8 ? 2 : 1))) void gemm_lnch_kernel(const float* X, const uint16_t* __restrict__ Wp, int ldp,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ ln,
-                                                         const float* __restrict__ geo, float* h, int ne) {
+                                                         const float* __restrict__ geo, float* h, int ne,
+                                                         const float* __restrict__ W0f, int n_up) {
   constexpr int C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, K = LN_D, BK = LN_BK, NK = K / BK;
   constexpr int ROWS = EPT * C;                    // activation rows per tile
   constexpr int NT = NWV * 64, CB = D / (16 * NWV);  // threads; 16-column blocks per wave
@@ -397,7 +398,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       }
     }
   };
-  if (MODE == 0 || !LNCH_RDMA_LATE) {
+  // MODE 0 of layer 1 (W0f): the residual h0 = f W0 is formed from the walkers' geometry in the
+  // epilogue (round 5), so h0 is never written by the input kernel nor read back here
+  constexpr bool fres = MODE == 0 && FRES;
+  if ((MODE == 0 || !LNCH_RDMA_LATE) && !fres) {
     rdma(0);
     if (NCHK > 1) rdma(1);
   }
@@ -504,7 +508,42 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     rdma(0);
     if (NCHK > 1) rdma(1);
   }
-  {
+  if constexpr (fres) {
+    // input.hip's channel features of this lane's electron (the geometry staged in gl) times
+    // W0's columns nf + 16 cb .. + 3, the input kernel's expression, then added as the
+    // residual rows are (r + acc)
+    const float4 g4 = gl[valid ? E - (e0 / N) * N : 0];  // st ct sp cp
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const int ie = (valid ? E : e0) % N;
+    const float rx = st * cp, ry = st * sp, rz = ct;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const float4 w0 = *reinterpret_cast<const float4*>(W0f + nf + 16 * cb);
+      const float4 w1 = *reinterpret_cast<const float4*>(W0f + D + nf + 16 * cb);
+      const float4 w2 = *reinterpret_cast<const float4*>(W0f + 2 * D + nf + 16 * cb);
+      const float4 w3 = *reinterpret_cast<const float4*>(W0f + 3 * D + nf + 16 * cb);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c == 0) {
+          f = make_float4(rz, rx, ry, (ie < n_up) ? 1.f : -1.f);
+        } else if (c <= T) {
+          const int t = c - 1;
+          if ((t >> 1) == ie) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
+        } else if (c == T + 1) {
+          f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
+        } else {
+          const int k = c - T - 2;  // 0:x 1:y 2:z
+          f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
+        }
+        f32x4& a = acc[c][cb];
+        a[0] = (f.x * w0.x + f.y * w1.x + f.z * w2.x + f.w * w3.x) + a[0];
+        a[1] = (f.x * w0.y + f.y * w1.y + f.z * w2.y + f.w * w3.y) + a[1];
+        a[2] = (f.x * w0.z + f.y * w1.z + f.z * w2.z + f.w * w3.z) + a[2];
+        a[3] = (f.x * w0.w + f.y * w1.w + f.z * w2.w + f.w * w3.w) + a[3];
+      }
+    }
+  } else {
     // this lane's row in a chunk buffer (+ channel / buffer offsets) and its two quad slots
     const char* const rb0 = smem + l16e * D * 4;
     int rsl[CB];
@@ -545,6 +584,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     LNCH_T(3);
   }
 #else
+  static_assert(!fres, "the feature residual needs the LNCH_RDMA build (the default)");
   {
     // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
     // hoisting all C * CB of them, which would spill the accumulators)
@@ -719,24 +759,28 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 
 template <int N, int NWV>
 void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s) {
+                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
   const size_t smem = lnch_smem(N);
   const int grid = (ne + LN_EPT - 1) / LN_EPT;
-  if (mode == 0) {
+  if (mode == 0 && W0f) {
+    ensure_smem(gemm_lnch_kernel<N, 0, NWV, true>, smem);
+    hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV, true>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo,
+                       h, ne, W0f, n_up);
+  } else if (mode == 0) {
     ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);
     hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne);
+                       ne, W0f, n_up);
   } else {
     ensure_smem(gemm_lnch_kernel<N, 1, NWV>, smem);
     hipLaunchKernelGGL((gemm_lnch_kernel<N, 1, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne);
+                       ne, nullptr, 0);
   }
 }
 
 template <int N>
 void launch_lnch_n(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s) {
-  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s);
+                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
+  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up);
 }
 
 }  // namespace
@@ -770,14 +814,15 @@ bool gemm_lnch_supported(int N, int D) {
 }
 
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                      const float* geo, float* h, int ne, int mode, hipStream_t s) {
+                      const float* geo, float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
+  if (mode != 0) W0f = nullptr;
   switch (N) {
-    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
-    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
-    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
-    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
-    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
-    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s); return;
+    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
   }
 }
 
