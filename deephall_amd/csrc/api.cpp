@@ -688,12 +688,16 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
                     gemm_lnch_supported(d.N, D);
   // local energy, gemm_lnch: layer 1's residual h0 = f W0 is formed in the first launch's
   // epilogue from geo (DH_LNCH_FEAT=0 keeps the input kernel writing h0)
-  const bool lnch_feat = lnch && d.L > 0 && lnch_feat_enabled();
+  const bool lnch_feat = lnch && fused && lnch_feat_enabled();  // fused: the input kernel writes no q|k|v
+  // local energy at N = 10, 20 (GEMM + layernorm_ch_quad): the same residual formed by the
+  // first LayerNorm launch, the GEMM writing t without it
+  const bool ln_feat = C > 1 && !lnch && !chain_ch && fused && D == 256 && (d.N == 10 || d.N == 20) &&
+                       lnch_feat_enabled();
   {
     const bool wq = fold && !fused;
     if (!(geo_ready && h_feat && !wq)) {
       PROF(PK_INPUT + (C > 1 ? PK_CH : 0), 8.0 * R * DD * (wq ? 4 : 1), f4 * R * DD * (wq ? 4 : 1));
-      launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, (h_feat || lnch_feat) ? nullptr : w.h,
+      launch_input(d, x, P.W0, wq ? P.W0qkv : nullptr, wq ? P.layer[0].bqkv : nullptr, (h_feat || lnch_feat || ln_feat) ? nullptr : w.h,
                    wq ? w.qkv : nullptr, w.geo, nw, C, s);
     }
   }
@@ -769,11 +773,13 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       }
       continue;
     }
-    // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded)
-    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, w.h, D, w.t, D, D, D);
+    // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded);
+    // layer 1 with ln_feat: t = o (Wo Wl) + bo Wl, the LayerNorm adds h0 = f W0
+    const bool lf = ln_feat && l == 0;
+    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, lf ? nullptr : w.h, D, w.t, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
-      launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s);
+      launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s, lf ? P.W0 : nullptr);
     }
     gemm(w.h, D, lp.Wm, lp.WmT, lp.WmP, D, lp.bm, nullptr, 0, w.o, D, D, D);
     {

@@ -179,7 +179,8 @@ void launch_lowrank_qk(const Dims& d, const float* W0qkv, const float* bqkv, flo
 //   mode 0: h = LN_ch(X)           (X may alias h)
 //   mode 1: h = LN_ch(h + tanh_ch(Z))
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
-                      int nw, int C, int mode, hipStream_t s);
+                      int nw, int C, int mode, hipStream_t s,
+                      const float* W0f = nullptr);
 
 // det.hip
 //   value mode (C == 1): logpsi[nw][2]

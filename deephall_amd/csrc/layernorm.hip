@@ -276,7 +276,7 @@ template <int N>
 __global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, const float* __restrict__ Z,
                                                                 const float* __restrict__ ln,
                                                                 const float* __restrict__ geo, float* h, int ne,
-                                                                int mode) {
+                                                                int mode, const float* __restrict__ W0f, int n_up) {
   constexpr int T = 2 * N, C = 2 * N + 5, D = 256, NR = C + T + 3;
   __shared__ float red[4][C + NR];
   __shared__ float al[3][T];       // flow coefficients (broadcast reads)
@@ -317,7 +317,31 @@ __global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, 
   };
   const size_t r0 = (size_t)e * C * D + 64 * w + lane;  // (row e*C, this lane's column)
   float z[C];
-  if (mode == 0) {
+  if (mode == 0 && W0f) {
+    // layer 1 (round 5): the residual h0 = f W0 of input.hip formed here from the geometry
+    // (the GEMM wrote t without it): z_c = t_c + f_c . W0[:, col], the GEMM epilogue's sum order
+    const int col = 64 * w + lane, i = e - b * N;
+    const float w0 = W0f[col], w1 = W0f[D + col], w2 = W0f[2 * D + col], w3 = W0f[3 * D + col];
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)e);  // st ct sp cp
+    const float st = g.x, ct = g.y, sp = g.z, cp = g.w;
+    const float rx = st * cp, ry = st * sp, rz = ct;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c == 0) {
+        f = make_float4(rz, rx, ry, (i < n_up) ? 1.f : -1.f);
+      } else if (c <= T) {
+        const int t = c - 1;
+        if ((t >> 1) == i) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
+      } else if (c == T + 1) {
+        f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
+      } else {
+        const int k = c - T - 2;  // 0:x 1:y 2:z
+        f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
+      }
+      z[c] = X[r0 + (size_t)c * D] + (f.x * w0 + f.y * w1 + f.z * w2 + f.w * w3);
+    }
+  } else if (mode == 0) {
 #pragma unroll
     for (int c = 0; c < C; ++c) z[c] = X[r0 + (size_t)c * D];
   } else {
@@ -428,15 +452,18 @@ void launch_ln_wave(const float* X, const float* Z, const float* ln, const float
 }  // namespace
 
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
-                      int nw, int C, int mode, hipStream_t s) {
+                      int nw, int C, int mode, hipStream_t s, const float* W0f) {
+  if (W0f && !(C > 1 && d.D == 256 && (d.N == 10 || d.N == 20) && mode == 0)) W0f = nullptr;  // quad kernel only
   if (C > 1 && d.D == 256 && (d.N <= 8 || d.N == 10 || d.N == 20)) {
     const int ne = nw * d.N;
     switch (d.N) {
       case 10:
-        hipLaunchKernelGGL(layernorm_ch_quad_kernel<10>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode);
+        hipLaunchKernelGGL(layernorm_ch_quad_kernel<10>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode, W0f,
+                           d.n_up);
         return;
       case 20:
-        hipLaunchKernelGGL(layernorm_ch_quad_kernel<20>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode);
+        hipLaunchKernelGGL(layernorm_ch_quad_kernel<20>, dim3(ne), dim3(256), 0, s, X, Z, ln, geo, h, ne, mode, W0f,
+                           d.n_up);
         return;
       case 1: launch_ln_wave<1>(X, Z, ln, geo, h, ne, mode, s); return;
       case 2: launch_ln_wave<2>(X, Z, ln, geo, h, ne, mode, s); return;

@@ -31,6 +31,7 @@ namespace {
 constexpr int kNT = 1024;
 constexpr int kNW = kNT / 64;
 constexpr int kMaxParts = 5;
+constexpr int kCache = 8;  // values per thread held in registers by iqr_bounds (B <= 8192)
 
 // order-preserving float -> uint32 (NaN excluded by the caller)
 __device__ __forceinline__ uint32_t fkey(float v) {
@@ -80,10 +81,35 @@ struct SelectLds {
 // stats_kernel, ROCm 7.2 clang -O2/-O3 crashes in instruction selection.)
 __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the order-preserving keys of this thread's values, read once (B <= kCache * kNT): the
+  // passes below then run on registers instead of re-reading global memory between atomics
+  const bool cached = B <= kCache * kNT;
+  uint32_t kc[kCache][kMaxParts];
+  uint64_t okm = 0;  // bit u * kMaxParts + p: value (u, p) is not NaN
+  if (cached) {
+#pragma unroll
+    for (int u = 0; u < kCache; ++u) {
+      const int i = tid + u * kNT;
+#pragma unroll
+      for (int p = 0; p < kMaxParts; ++p) {
+        const float v = (p < np && i < B) ? part_value(s, p, i) : NAN;
+        const bool ok = !isnan(v);
+        kc[u][p] = ok ? fkey(v) : 0u;
+        if (ok) okm |= 1ull << (u * kMaxParts + p);
+      }
+    }
+  }
   // valid counts
   int c[kMaxParts] = {0, 0, 0, 0, 0};
-  for (int i = tid; i < B; i += kNT)
-    for (int p = 0; p < np; ++p) c[p] += isnan(part_value(s, p, i)) ? 0 : 1;
+  if (cached) {
+#pragma unroll
+    for (int u = 0; u < kCache; ++u)
+#pragma unroll
+      for (int p = 0; p < kMaxParts; ++p) c[p] += (okm >> (u * kMaxParts + p)) & 1ull ? 1 : 0;
+  } else {
+    for (int i = tid; i < B; i += kNT)
+      for (int p = 0; p < np; ++p) c[p] += isnan(part_value(s, p, i)) ? 0 : 1;
+  }
   for (int p = 0; p < np; ++p) {
     int v = c[p];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -110,12 +136,7 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
     const uint32_t hmask = pass == 0 ? 0u : (0xffffffffu << (shift + 8));
     for (int j = tid; j < nh * 256; j += kNT) (&L.hist[0][0])[j] = 0u;
     __syncthreads();
-    for (int i0 = 0; i0 < B; i0 += kNT) {
-      const int i = i0 + tid;
-      for (int p = 0; p < np; ++p) {
-        const float v = i < B ? part_value(s, p, i) : NAN;
-        const bool ok = !isnan(v);
-        const uint32_t u = ok ? fkey(v) : 0u;
+    auto count = [&](bool ok, uint32_t u, int p) __attribute__((always_inline)) {
         const uint32_t dig = (u >> shift) & 255u;
         for (int r = 0; r < 4; ++r) {
           const bool take = ok && ((u ^ L.prefix[4 * p + r]) & hmask) == 0u;
@@ -128,6 +149,23 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
           const uint64_t same = __ballot(take && dig == ldig);
           if (lane == lead) atomicAdd(&L.hist[4 * p + r][ldig], (uint32_t)__popcll(same));
           if (take && dig != ldig) atomicAdd(&L.hist[4 * p + r][dig], 1u);
+        }
+    };
+    if (cached) {
+#pragma unroll
+      for (int u = 0; u < kCache; ++u) {
+        if (u * kNT >= B) break;  // block-uniform
+#pragma unroll
+        for (int p = 0; p < kMaxParts; ++p)
+          if (p < np) count((okm >> (u * kMaxParts + p)) & 1ull, kc[u][p], p);
+      }
+    } else {
+      for (int i0 = 0; i0 < B; i0 += kNT) {
+        const int i = i0 + tid;
+        for (int p = 0; p < np; ++p) {
+          const float v = i < B ? part_value(s, p, i) : NAN;
+          const bool ok = !isnan(v);
+          count(ok, ok ? fkey(v) : 0u, p);
         }
       }
     }
