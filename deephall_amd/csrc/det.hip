@@ -1497,8 +1497,16 @@ __host__ __device__ inline DetWaveSmem det_wave_layout(int N, int M, int K) {
 }
 constexpr int kDetWaveMaxN = 8;
 
+#ifndef DET_WAVE_WPE  // A/B knob: waves per SIMD the det_energy_wave_kernel is compiled for (0: the compiler's choice)
+#define DET_WAVE_WPE 0
+#endif
+#if DET_WAVE_WPE > 0
+#define DET_WAVE_ATTR __attribute__((amdgpu_waves_per_eu(DET_WAVE_WPE, DET_WAVE_WPE)))
+#else
+#define DET_WAVE_ATTR
+#endif
 template <int NV, bool VEC>
-__global__ __launch_bounds__(64) void det_energy_wave_kernel(const float* __restrict__ Fp, int ldF,
+__global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const float* __restrict__ Fp, int ldF,
                                                              const float* __restrict__ x, const float* __restrict__ geo_g,
                                                              const float* __restrict__ jas, const float* __restrict__ norm,
                                                              float* __restrict__ e_l, float* __restrict__ obs, int N,

@@ -2526,43 +2526,78 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   CHAIN_T(1);
   gemm(NoTr{});
   CHAIN_T(2);
-  prefetch(a.Wp2, a.ldp2, 0);
   {
-    float4 w0[4][4];  // feature residual: W0 rows at this lane's columns
+    // every load of this phase issued before the first use, and P2's weight prefetch after
+    // them (round 5): left to the compiler the bias / geometry loads went out one or two at a
+    // time, each behind a vmcnt(0) that also waited for the weight prefetch (14 serialised
+    // round trips per tile)
+    float4 bvv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bvv[g] = *reinterpret_cast<const float4*>(a.b1 + colof(g));
     if (a.feat.W0) {
+      float4 w0[4][4];  // feature residual: W0 rows at this lane's columns
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int q = 0; q < 4; ++q) w0[g][q] = *reinterpret_cast<const float4*>(a.feat.W0 + q * CH_BN + colof(g));
-    }
+      float4 gq[RB];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int r = row0 + 32 * rb + l32;
-      float f[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.feat.W0 && r < rows) {  // geo holds exactly rows entries
-        const float4 gq = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
-        f[0] = gq.y;
-        f[1] = gq.x * gq.w;
-        f[2] = gq.x * gq.z;
-        f[3] = (r % a.feat.N < a.feat.n_up) ? 1.f : -1.f;
+      for (int rb = 0; rb < RB; ++rb) {  // geo holds exactly rows entries: clamped, masked below
+        const int r = min(row0 + 32 * rb + l32, rows - 1);
+        gq[rb] = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
       }
+      __builtin_amdgcn_sched_barrier(0);  // the residual loads ahead of the prefetch in vmcnt's queue
+      prefetch(a.Wp2, a.ldp2, 0);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 bv = *reinterpret_cast<const float4*>(a.b1 + colof(g));
-        float4 rv;
-        if (a.feat.W0) {
+      for (int rb = 0; rb < RB; ++rb) {
+        const int r = row0 + 32 * rb + l32;
+        float f[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r < rows) {
+          f[0] = gq[rb].y;
+          f[1] = gq[rb].x * gq[rb].w;
+          f[2] = gq[rb].x * gq[rb].z;
+          f[3] = (r % a.feat.N < a.feat.n_up) ? 1.f : -1.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = bvv[g];
+          float4 rv;
           rv.x = f[0] * w0[g][0].x + f[1] * w0[g][1].x + f[2] * w0[g][2].x + f[3] * w0[g][3].x;
           rv.y = f[0] * w0[g][0].y + f[1] * w0[g][1].y + f[2] * w0[g][2].y + f[3] * w0[g][3].y;
           rv.z = f[0] * w0[g][0].z + f[1] * w0[g][1].z + f[2] * w0[g][2].z + f[3] * w0[g][3].z;
           rv.w = f[0] * w0[g][0].w + f[1] * w0[g][1].w + f[2] * w0[g][2].w + f[3] * w0[g][3].w;
-        } else {
-          rv = *reinterpret_cast<const float4*>(a.h + (size_t)r * CH_BN + colof(g));  // h padded to 768 rows
+          x[rb][4 * g] = (acc[rb][4 * g] + bv.x) + rv.x;
+          x[rb][4 * g + 1] = (acc[rb][4 * g + 1] + bv.y) + rv.y;
+          x[rb][4 * g + 2] = (acc[rb][4 * g + 2] + bv.z) + rv.z;
+          x[rb][4 * g + 3] = (acc[rb][4 * g + 3] + bv.w) + rv.w;
         }
-        x[rb][4 * g] = (acc[rb][4 * g] + bv.x) + rv.x;
-        x[rb][4 * g + 1] = (acc[rb][4 * g + 1] + bv.y) + rv.y;
-        x[rb][4 * g + 2] = (acc[rb][4 * g + 2] + bv.z) + rv.z;
-        x[rb][4 * g + 3] = (acc[rb][4 * g + 3] + bv.w) + rv.w;
       }
+    } else {
+      // the residual rows of h straight into x, then x = (acc + b) + h (the same sum)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const int r = row0 + 32 * rb + l32;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 rv = *reinterpret_cast<const float4*>(a.h + (size_t)r * CH_BN + colof(g));  // h padded to 768 rows
+          x[rb][4 * g] = rv.x;
+          x[rb][4 * g + 1] = rv.y;
+          x[rb][4 * g + 2] = rv.z;
+          x[rb][4 * g + 3] = rv.w;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      prefetch(a.Wp2, a.ldp2, 0);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = bvv[g];
+          x[rb][4 * g] = (acc[rb][4 * g] + bv.x) + x[rb][4 * g];
+          x[rb][4 * g + 1] = (acc[rb][4 * g + 1] + bv.y) + x[rb][4 * g + 1];
+          x[rb][4 * g + 2] = (acc[rb][4 * g + 2] + bv.z) + x[rb][4 * g + 2];
+          x[rb][4 * g + 3] = (acc[rb][4 * g + 3] + bv.w) + x[rb][4 * g + 3];
+        }
     }
   }
   CHAIN_T(3);
