@@ -58,6 +58,9 @@
 #ifndef LNCH_OPQ
 #define LNCH_OPQ 1
 #endif
+#ifndef LNCH_LBAR  // A/B knob: barriers that wait for LDS only (lgkmcnt(0) + s_barrier), round 5: __syncthreads'
+#define LNCH_LBAR 1  // vmcnt(0) drained the next k-step's activation loads every step and the next residual chunk
+#endif
 #ifndef LNCH_RPF
 #define LNCH_RPF 0
 #endif
@@ -163,6 +166,17 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, kg = lane >> 4;
   const int tile = blockIdx.x;
+  // every barrier here orders LDS only (planes, residual chunks after their counted DMA waits,
+  // statistics): global loads in flight may cross it
+  auto lbar = []() __attribute__((always_inline)) {
+#if LNCH_LBAR
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+  };
   const int e0 = tile * EPT;                       // first electron of the tile
   const size_t row0 = (size_t)e0 * C;
   const int rows_valid = min(ROWS, (ne - e0) * C);
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     load_a(1, ra);
 #pragma unroll 1
     for (int kt = 0; kt < NK; ++kt) {
-      __syncthreads();  // planes of step kt complete; step kt - 1's buffer is free
+      lbar();  // planes of step kt complete; step kt - 1's buffer is free
       const char* P = smem + (kt & 1) * STAGE + xoff;
       if (kt + 1 < NK) {
 #pragma unroll
@@ -304,7 +318,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     load_a(1, ra);
 #pragma unroll 1
     for (int kt = 0; kt < NK; ++kt) {
-      __syncthreads();  // planes of step kt complete; step kt - 1's buffer is free
+      lbar();  // planes of step kt complete; step kt - 1's buffer is free
       if (kt == 0) LNCH_T(1);
       const char* P = smem + (kt & 1) * STAGE + xoff;
 #pragma unroll
@@ -358,7 +372,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     if (MODE == 0 && LNCH_RPF && (rpf ^ rpv) == 0x7fc00001u && ne < 0) h[0] = 0.f;  // never taken
   }
 #endif
-  __syncthreads();  // every wave is past its last plane read: the stage buffers become scratch
+  lbar();  // every wave is past its last plane read: the stage buffers become scratch
   LNCH_T(2);
   // the epilogue's lane indices, re-derived from the lane id (mbcnt) rather than kept live
   // across the k loop from threadIdx (holding them there made MODE 1 spill)
@@ -556,7 +570,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(rows_of(k + 1) / NWV) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      lbar();
 #pragma unroll
       for (int cc = 0; cc < LN_RCH; ++cc) {
         const int c = LN_RCH * k + cc;
@@ -576,11 +590,11 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         }
       }
       if (k + 2 < NCHK) {
-        __syncthreads();  // every wave is done with buffer k & 1
+        lbar();  // every wave is done with buffer k & 1
         rdma(k + 2);
       }
     }
-    __syncthreads();  // the chunk buffers become the statistics scratch
+    lbar();  // the chunk buffers become the statistics scratch
     LNCH_T(3);
   }
 #else
@@ -628,7 +642,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #endif
       __builtin_amdgcn_sched_barrier(0);          // one statistic at a time (register pressure)
     }
-    __syncthreads();
+    lbar();
     for (int i = tide; i < NS * EPT; i += NT) {
       const int j = i / EPT, e = i - j * EPT;
       float s = 0.f;
@@ -638,7 +652,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         for (int g = 0; g < (LNCH_PERMLANE ? 1 : 4); ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
       tot[e * TS + j] = s * (1.f / D);
     }
-    __syncthreads();
+    lbar();
   };
   const float* mt = tot + l16e * TS;  // this lane's electron
   // channel means, centre
