@@ -74,6 +74,19 @@ __device__ __forceinline__ f4v feat_channel(int c, int i, float4 g, float spin) 
 
 // FEAT (layer 1): the q|k|v rows are formed from the K = 4 input features and the folded
 // W0 Wqkv (+ the bias on the value channel) in the prefetch, instead of read from memory.
+#ifndef ATTN_MFMA_LBAR  // A/B knob: the barriers wait for LDS only (1); __syncthreads' vmcnt(0) drained the
+#define ATTN_MFMA_LBAR 1  // next channels' q|k|v prefetch at every one of them (0)
+#endif
+__device__ __forceinline__ void mbar() {
+#if ATTN_MFMA_LBAR
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 template <int N, bool FEAT>
 __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ qkv,
                                                              const float* __restrict__ geo, float* __restrict__ o,
@@ -215,13 +228,13 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
   prefetch(0);
   commit(S0);
   prefetch(1);
-  __syncthreads();
+  mbar();
   {
     f4v acc = {0.f, 0.f, 0.f, 0.f};
     acc = dot64(S0, S0 + N * LD, arow, brow, acc);
     store_scores(acc);
   }
-  __syncthreads();
+  mbar();
   if (erow) {
     float sv[JU], mx = -INFINITY;
 #pragma unroll
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
   }
   commit(bufof(1));  // channel 1 (its buffer is untouched so far)
   prefetch(2);
-  __syncthreads();
+  mbar();
   float* obase = o + (size_t)b * N * C * D + h * 64 + 16 * w + r16;
   auto store_out = [&](int c, int I, f4v acc) __attribute__((always_inline)) {
 #pragma unroll
@@ -291,7 +304,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     const float* KC = buf + N * LD;
     const float* VC = buf + 2 * N * LD;
     float* FS = sm + L::oB2;  // flow set (Qu_k | Ku_k | Vu_k) for c >= T + 2
-    __syncthreads();  // B1: channel c committed (and, for a flow channel, its flow set)
+    mbar();  // B1: channel c committed (and, for a flow channel, its flow set)
     // phase 1: scores
     {
       f4v acc = {0.f, 0.f, 0.f, 0.f};
@@ -310,7 +323,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
       }
       store_scores(acc);
     }
-    __syncthreads();  // B2
+    mbar();  // B2
     // phase 2: softmax derivative -> AT; accumulators
     if (erow) {
       float sv[JU], pv[JU], a0[JU], m1 = 0.f, m2 = 0.f;
@@ -370,7 +383,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         }
       }
     }
-    __syncthreads();  // B3: AT complete
+    mbar();  // B3: AT complete
     // the next channel's rows into the other buffer (its last readers finished before B1)
     const bool next_flow = c + 1 >= T + 2;
     if (c + 1 < C && !next_flow) {
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     if (c + 1 < C && next_flow) {
       // flow channel k = c + 1 - T - 2: single-buffered (B1 <- its rows, B2 <- the flow set)
       const int k = c + 1 - T - 2;
-      __syncthreads();  // B4: every reader of B1 / B2 / AU is done
+      mbar();  // B4: every reader of B1 / B2 / AU is done
       commit(sm + L::oB1);
       if (c + 2 < C) prefetch(c + 2);
 #pragma unroll

@@ -129,20 +129,25 @@ __host__ __device__ constexpr int attn_feat_floats() { return N * N; }
 // NT walkers b0 .. b0 + NT - 1 of one head (Mh: its 25 Mqk entries, row-major); pv: this lane's
 // column of v per task and electron (feat_qkv); st: NT x attn_feat_floats(N) floats of
 // wave-private LDS; out[t][i] = o of task t, electron i, column d = lane.
-template <int N, int NT>
-__device__ __forceinline__ void attn_feat_core(const float* __restrict__ Mh, const float* __restrict__ geo, int b0,
-                                               int n_up, const float (&pv)[NT][N], float* st, int lane,
-                                               float (&out)[NT][N]) {
+// geo_at(row): the (st, ct, sp cp) float4 of electron row (global memory or a staged copy)
+template <int N, int NT, class GeoAt>
+__device__ __forceinline__ void attn_feat_core_g(const float (&M)[25], GeoAt geo_at, int b0, int n_up,
+                                                 const float (&pv)[NT][N], float* st, int lane, float (&out)[NT][N]) {
   constexpr int nn = N * N, PER = attn_feat_floats<N>();
-  float M[25];
-#pragma unroll
-  for (int q = 0; q < 25; ++q) M[q] = Mh[q];
+  auto feat5g = [&](int row, bool up, float (&f)[5]) __attribute__((always_inline)) {
+    const float4 g = geo_at(row);  // st ct sp cp
+    f[0] = g.y;
+    f[1] = g.x * g.w;
+    f[2] = g.x * g.z;
+    f[3] = up ? 1.f : -1.f;
+    f[4] = 1.f;
+  };
   __builtin_amdgcn_wave_barrier();  // a previous call's readers of st (LDS ops of a wave run in order)
   for (int p = lane; p < NT * nn; p += 64) {
     const int t = p / nn, pair = p - t * nn, i = pair / N, j = pair - (pair / N) * N;
     float fi[5], fj[5];
-    feat5(geo, (b0 + t) * N + i, i < n_up, fi);
-    feat5(geo, (b0 + t) * N + j, j < n_up, fj);
+    feat5g((b0 + t) * N + i, i < n_up, fi);
+    feat5g((b0 + t) * N + j, j < n_up, fj);
     float s = 0.f;
 #pragma unroll
     for (int a = 0; a < 5; ++a) {
@@ -184,15 +189,31 @@ __device__ __forceinline__ void attn_feat_core(const float* __restrict__ Mh, con
   }
 }
 
+template <int N, int NT>
+__device__ __forceinline__ void attn_feat_core(const float* __restrict__ Mh, const float* __restrict__ geo, int b0,
+                                               int n_up, const float (&pv)[NT][N], float* st, int lane,
+                                               float (&out)[NT][N]) {
+  float M[25];
+#pragma unroll
+  for (int q = 0; q < 25; ++q) M[q] = Mh[q];
+  attn_feat_core_g<N, NT>(
+      M, [&](int row) { return *reinterpret_cast<const float4*>(geo + 4 * (size_t)row); }, b0, n_up, pv, st, lane,
+      out);
+}
+
 // this lane's column of v only (feat_qkv without q and k: the scores come from Mqk)
-template <int N>
-__device__ __forceinline__ void feat_v(const FeatW& fw, const float* __restrict__ geo, int b, int n_up, float (&pv)[N]) {
+template <int N, class GeoAt>
+__device__ __forceinline__ void feat_v_g(const FeatW& fw, GeoAt geo_at, int b, int n_up, float (&pv)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));
+    const float4 g = geo_at(b * N + i);
     const float4 f = make_float4(g.y, g.x * g.w, g.x * g.z, (i < n_up) ? 1.f : -1.f);
     pv[i] = FeatW::dot(f, fw.wv) + fw.bv;
   }
+}
+template <int N>
+__device__ __forceinline__ void feat_v(const FeatW& fw, const float* __restrict__ geo, int b, int n_up, float (&pv)[N]) {
+  feat_v_g<N>(fw, [&](int row) { return *reinterpret_cast<const float4*>(geo + 4 * (size_t)row); }, b, n_up, pv);
 }
 
 }  // namespace dh

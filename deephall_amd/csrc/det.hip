@@ -647,6 +647,18 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
 // on harmonics MW w + g + G u (u < MG); the channel loop is unrolled (C compile-time) so the
 // register ring is indexed by constants.  The leaves, the per-row sums, the lane-group and
 // cross-wave reductions and the PhiC layout are env_contract_kernel's (K = 1).
+#ifndef DET_WAVE_LBAR  // A/B knob: det_energy_wave_kernel's channel-loop barriers wait for LDS only (1) or
+#define DET_WAVE_LBAR 1  // are __syncthreads, whose vmcnt(0) drained the next channel's staging loads (0)
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if DET_WAVE_LBAR
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
 template <int N, int MG, int D>
 __global__ __launch_bounds__(256, 2) void env_stream_kernel(const float* __restrict__ Fp, int ldF,
                                                             const float* __restrict__ x,
@@ -722,7 +734,7 @@ __global__ __launch_bounds__(256, 2) void env_stream_kernel(const float* __restr
       al[2 * T + tid] = (tid & 1) ? ga.x : 0.f;
     }
   }
-  __syncthreads();
+  lds_barrier();  // the leaves are LDS; the D rows requested above stay in flight across it
   // the envelope factors are re-read from LDS per row (the index is laundered so that they are
   // not hoisted into registers: the VGPRs go to rows in flight instead)
   // per-row result store without a branch (a branch per row splits the unrolled bodies into
@@ -804,7 +816,7 @@ __global__ __launch_bounds__(256, 2) void env_stream_kernel(const float* __restr
     const cf v{gsum(e0a.re), gsum(e0a.im)};
     dst[c * dstride] = v;
   }
-  __syncthreads();
+  lds_barrier();
   float* out = PhiC + 2 * ((size_t)b * C * N * N + (size_t)i * N);
   for (int e = tid; e < C * N; e += 256) {
     const int c = e / N, jj = e - (e / N) * N;
@@ -1636,10 +1648,11 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
     cf Gu[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}}, LB2{0.f, 0.f}, PL{0.f, 0.f};
     cf PS[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
     for (int c = 0; c < C; ++c) {
-      __syncthreads();  // the readers of channel c - 1 are done with Fs
+      lds_barrier();  // the readers of channel c - 1 are done with Fs
       stage_store();
-      __syncthreads();
-      if (c + 1 < C) stage_load(c + 1);  // in flight while channel c is contracted
+      lds_barrier();
+      if (c + 1 < C) stage_load(c + 1);  // in flight while channel c is contracted (and across
+                                         // the next barriers: they wait for LDS only, round 5)
       if (c == 0) {
         for (int m = 0; m < M; ++m) {
           const cf f{Frow[m * NK], Frow[MNK + m * NK]};

@@ -114,17 +114,34 @@ constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
 constexpr int LN_D = 256;   // features (= K)
 constexpr int LN_BK = 32;   // k per step
 // epilogue residual through LDS (LNCH_RDMA): chunks of LN_RCH channel rows of all 16
-// electrons (LN_RCH * 16 rows of 1 KB), two chunk buffers
-constexpr int LN_RCH = 4;
+// electrons (LN_RCH * 16 rows of 1 KB).  LNCH_R3 (round 5): 3-row chunks in three buffers —
+// two over the stage area, the third past the geometry, free during the k loop, so chunk 0 is
+// requested at kernel start (its latency hides behind the first k-step's own loads) and two
+// chunks are in flight behind the one being added; else 4-row chunks in two buffers
+#ifndef LNCH_R3
+#define LNCH_R3 0  // measured neutral (profiles/r05_v13_ab.txt): kept off
+#endif
+constexpr int LN_RCH = LNCH_R3 ? 3 : 4;
+constexpr int LN_NBUF = LNCH_R3 ? 3 : 2;
 constexpr int LN_RBUF = LN_RCH * LN_EPT * LN_D * 4;  // bytes of one chunk buffer
 
 // LDS bytes of the kernel: the two k-step plane stages (reused by the epilogue's residual
-// chunks and statistics), then the walkers' geometry
+// chunks and statistics), then the walkers' geometry, then (LNCH_R3) the third chunk buffer
 __host__ __device__ constexpr int lnch_geo_off(int N) {
   return (6 * (2 * N + 5) * LN_EPT * 64 > (LNCH_RDMA ? 2 * LN_RBUF : 0)) ? 6 * (2 * N + 5) * LN_EPT * 64
                                                                        : 2 * LN_RBUF;
 }
-__host__ __device__ constexpr int lnch_smem(int N) { return lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16; }
+__host__ __device__ constexpr int lnch_bx_off(int N) {
+  return (lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16 + 1023) & ~1023;
+}
+__host__ __device__ constexpr int lnch_smem(int N) {
+  return (LNCH_RDMA && LN_NBUF == 3) ? lnch_bx_off(N) + LN_RBUF
+                                     : lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16;
+}
+// byte offset of chunk k's buffer
+__host__ __device__ constexpr int lnch_cbuf(int N, int k) {
+  return LN_NBUF == 3 ? (k % 3 == 0 ? lnch_bx_off(N) : (k % 3 - 1) * LN_RBUF) : (k & 1) * LN_RBUF;
+}
 
 __device__ __forceinline__ uint32_t pkbf(float x, float y) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
@@ -236,6 +253,48 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   };
   const int xoff = l16 * 64 + ((kg ^ lnch_sw(l16)) * 16);  // + c * EPT * 64 within a plane
 
+#if LNCH_RDMA
+  // ---- the residual rows h through LDS by DMA (global_load_lds_dwordx4, no VGPRs): chunk k =
+  // channel rows LN_RCH k .. + LN_RCH - 1 of the tile's 16 electrons, one 1-KB row per wave
+  // instruction, into chunk buffer lnch_cbuf(k) at row q = (c - LN_RCH k) * 16 + e.  16-B slot s of
+  // a row holds the row's quad s ^ e (the swizzle is on the SOURCE address: the DMA writes
+  // lane-linearly), so the epilogue's ds_read_b128 of quad Q = 8 w + 4 cb + g by lane (e, g)
+  // hits slot Q ^ e: 16 distinct slots in every lane group.  Rows of electrons past the end
+  // re-read the tile's first row into their (never read) slot, so every wave issues the same
+  // compile-time number of DMAs per chunk and "chunk k landed" is vmcnt(DMAs of the younger
+  // chunks k + 1 .. k + LN_NBUF - 1).
+  constexpr int NCHK = (C + LN_RCH - 1) / LN_RCH;
+  auto rows_of = [](int k) { return EPT * (C - LN_RCH * k < LN_RCH ? C - LN_RCH * k : LN_RCH); };
+  static_assert(EPT * LN_RCH % NWV == 0 && EPT % NWV == 0, "DMA rows must divide over the waves");
+  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
+  auto rdma = [&](int k) {
+    const int nrow = rows_of(k);
+#pragma unroll
+    for (int j = 0; j < LN_RCH * EPT / NWV; ++j) {
+      const int q = wid + NWV * j;  // wave-uniform
+      if (q < nrow) {
+        const int c = LN_RCH * k + q / EPT, e = q % EPT;
+        const int er = e0 + e < ne ? e : 0;
+        // row base in SGPRs, the lane's swizzled 16-B quad as a 32-bit VGPR offset (formed here,
+        // not hoisted: 64-bit per-lane addresses of every chunk held across the epilogue spill)
+        const float* rowp = h + (row0 + (size_t)(er * C + c)) * D;
+        const int le = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        uint32_t voff = (uint32_t)(le ^ e) << 4;
+        asm volatile("" : "+v"(voff));
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(lnch_cbuf(N, k) + q * D * 4));
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rowp), "s"(dst)
+                     : "memory");
+      }
+    }
+  };
+  // MODE 0 of layer 1 (W0f): the residual h0 = f W0 is formed from the walkers' geometry in the
+  // epilogue (round 5), so h0 is never written by the input kernel nor read back here
+  constexpr bool fres = MODE == 0 && FRES;
+  if (LN_NBUF == 3 && !fres) rdma(0);  // LNCH_R3: chunk 0 into the buffer past the stages, now
+#endif
   // the accumulators start from zero (the residual is added in the epilogue: starting them
   // from h rounds every k-step's partial sum at |h| and measurably loosened the tangent
   // channels against float64 on ill-conditioned walkers)
@@ -378,46 +437,11 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   // across the k loop from threadIdx (holding them there made MODE 1 spill)
   const int lane_e = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #if LNCH_RDMA
-  // ---- the residual rows h through LDS by DMA (global_load_lds_dwordx4, no VGPRs): chunk k =
-  // channel rows LN_RCH k .. + LN_RCH - 1 of the tile's 16 electrons, one 1-KB row per wave
-  // instruction, into chunk buffer k & 1 at row q = (c - LN_RCH k) * 16 + e.  16-B slot s of
-  // a row holds the row's quad s ^ e (the swizzle is on the SOURCE address: the DMA writes
-  // lane-linearly), so the epilogue's ds_read_b128 of quad Q = 8 w + 4 cb + g by lane (e, g)
-  // hits slot Q ^ e: 16 distinct slots in every lane group.  Rows of electrons past the end
-  // re-read the tile's first row into their (never read) slot, so every wave issues the same
-  // compile-time number of DMAs per chunk and "chunk k landed" is vmcnt(DMAs of chunk k + 1).
-  constexpr int NCHK = (C + LN_RCH - 1) / LN_RCH;
-  auto rows_of = [](int k) { return EPT * (C - LN_RCH * k < LN_RCH ? C - LN_RCH * k : LN_RCH); };
-  static_assert(EPT * LN_RCH % NWV == 0 && EPT % NWV == 0, "DMA rows must divide over the waves");
-  const uint32_t lds0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)smem);
-  auto rdma = [&](int k) {
-    const int nrow = rows_of(k);
-#pragma unroll
-    for (int j = 0; j < LN_RCH * EPT / NWV; ++j) {
-      const int q = wid + NWV * j;  // wave-uniform
-      if (q < nrow) {
-        const int c = LN_RCH * k + q / EPT, e = q % EPT;
-        const int er = e0 + e < ne ? e : 0;
-        // row base in SGPRs, the lane's swizzled 16-B quad as a 32-bit VGPR offset (formed here,
-        // not hoisted: 64-bit per-lane addresses of every chunk held across the epilogue spill)
-        const float* rowp = h + (row0 + (size_t)(er * C + c)) * D;
-        uint32_t voff = (uint32_t)(lane_e ^ e) << 4;
-        asm volatile("" : "+v"(voff));
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((k & 1) * LN_RBUF + q * D * 4));
-        unsigned keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(voff), "s"(rowp), "s"(dst)
-                     : "memory");
-      }
-    }
-  };
-  // MODE 0 of layer 1 (W0f): the residual h0 = f W0 is formed from the walkers' geometry in the
-  // epilogue (round 5), so h0 is never written by the input kernel nor read back here
-  constexpr bool fres = MODE == 0 && FRES;
   if ((MODE == 0 || !LNCH_RDMA_LATE) && !fres) {
-    rdma(0);
-    if (NCHK > 1) rdma(1);
+    if (LN_NBUF == 2) rdma(0);
+#pragma unroll
+    for (int x = 1; x < LN_NBUF; ++x)
+      if (x < NCHK) rdma(x);
   }
 #endif
   const int l16e = lane_e & 15, kge = lane_e >> 4, tide = wid * 64 + lane_e;
@@ -519,8 +543,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       for (int cb = 0; cb < CB; ++cb) asm volatile("" : "+v"(acc[c][cb]));
   }
   if (MODE == 1 && LNCH_RDMA_LATE) {
-    rdma(0);
-    if (NCHK > 1) rdma(1);
+    if (LN_NBUF == 2) rdma(0);
+#pragma unroll
+    for (int x = 1; x < LN_NBUF; ++x)
+      if (x < NCHK) rdma(x);
   }
   if constexpr (fres) {
     // input.hip's channel features of this lane's electron (the geometry staged in gl) times
@@ -565,9 +591,13 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     for (int cb = 0; cb < CB; ++cb) rsl[cb] = 16 * ((4 * CB * wid + 4 * cb + kge) ^ l16e);
 #pragma unroll
     for (int k = 0; k < NCHK; ++k) {
-      // this wave's chunk-k DMAs landed (the younger ones are chunk k + 1's), then every wave's
-      if (k + 1 < NCHK)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(rows_of(k + 1) / NWV) : "memory");
+      // this wave's chunk-k DMAs landed (the younger ones are chunks k + 1 .. k + LN_NBUF - 1,
+      // issued before this wait), then every wave's
+      const int YNG = (k + 1 < NCHK ? rows_of(k + 1) : 0) / NWV + (LN_NBUF == 3 && k + 2 < NCHK ? rows_of(k + 2) : 0) / NWV;
+      if (YNG > 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((k + 1 < NCHK ? rows_of(k + 1) : 0) / NWV +
+                                                (LN_NBUF == 3 && k + 2 < NCHK ? rows_of(k + 2) : 0) / NWV)
+                     : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lbar();
@@ -577,7 +607,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         if (c < C) {
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) {
-            const float4 r = *reinterpret_cast<const float4*>(rb0 + (k & 1) * LN_RBUF + cc * EPT * D * 4 + rsl[cb]);
+            const float4 r = *reinterpret_cast<const float4*>(rb0 + lnch_cbuf(N, k) + cc * EPT * D * 4 + rsl[cb]);
             f32x4& a = acc[c][cb];
             a[0] = r.x + a[0];
             a[1] = r.y + a[1];
@@ -589,9 +619,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           }
         }
       }
-      if (k + 2 < NCHK) {
-        lbar();  // every wave is done with buffer k & 1
-        rdma(k + 2);
+      if (k + LN_NBUF < NCHK) {
+        lbar();  // every wave is done with chunk k's buffer
+        rdma(k + LN_NBUF);
       }
     }
     lbar();  // the chunk buffers become the statistics scratch

@@ -54,6 +54,9 @@
 #ifndef CHAIN_P3T  // A/B knob: P3 MFMAs with the operands swapped (accumulator = tile row x 32 columns,
 #define CHAIN_P3T 1  // one register = two 128-B row segments: full-rate dword stores) instead of float4
 #endif               // stores of 32 rows x 32 B per instruction (round 5)
+#ifndef CHAIN_LBAR  // A/B knob: the chain kernel's barriers wait for LDS only (lgkmcnt(0) + s_barrier) instead
+#define CHAIN_LBAR 1  // of __syncthreads' vmcnt(0), which also waited for the next GEMM's weight prefetch (round 5)
+#endif
 #ifndef CHAIN_STAMP  // diagnostic builds only (tools/chain_stamp.py): per-tile phase stamps of chain_x6s
 #define CHAIN_STAMP 0
 #endif
@@ -2262,6 +2265,18 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
   }
   const int row0 = bid * CH_BM, rows = a.rows;
+  // every barrier of this kernel orders LDS only (planes, partial sums, staging); no wave reads
+  // global memory another wave of the launch wrote, so the VMEM queue (weight prefetch, h / Y3
+  // stores) may stay in flight across it
+  auto lbar = []() __attribute__((always_inline)) {
+#if CHAIN_LBAR
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+  };
   CHAIN_T(0);
   if (CHAIN_PRM) {  // read before the prologue's barrier
     for (int q = tid; q < 5 * 256; q += 512)
@@ -2388,7 +2403,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         part[(CS_NW + wid) * CH_BM + 32 * rb + l32] = q;
       }
     }
-    __syncthreads();
+    lbar();
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       float t = 0.f, q = 0.f;
@@ -2420,7 +2435,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       t += __shfl_xor(t, 32, 64);
       if (lh == 0) part[wid * CH_BM + 32 * rb + l32] = t;
     }
-    __syncthreads();
+    lbar();
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       float t = 0.f;
@@ -2436,7 +2451,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       q += __shfl_xor(q, 32, 64);
       if (lh == 0) part[(CS_NW + wid) * CH_BM + 32 * rb + l32] = q;
     }
-    __syncthreads();
+    lbar();
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       float t = 0.f;
@@ -2469,6 +2484,20 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     FeatW fw;
     fw.load(a.feat.W0qkv, a.feat.bqkv, CH_K, hd * 64 + lane);
     const float* Mh = a.feat.Mqk + hd * kMqkStride;  // the head's score form (attn_feat_core)
+    // the geometry of this wave's WPW walkers, staged once in wave-private LDS past the
+    // staging areas (round 5: every attn_feat_core / feat_v call re-read it from global memory,
+    // a dependent round trip per call), and the head's score form in registers once
+    static_assert(WPW * NA <= 64 && CS_NW * (PER + 4 * WPW * NA) * 4 <= 3 * CS_PLANE, "geometry staging");
+    float4* gs = reinterpret_cast<float4*>(reinterpret_cast<float*>(smem) + CS_NW * PER) + wid * WPW * NA;
+    const int grow0 = row0 + wl0 * NA;  // first electron row of the wave's walkers
+    if (lane < WPW * NA)
+      gs[lane] = grow0 + lane < rows ? *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)(grow0 + lane))
+                                     : make_float4(0.f, 1.f, 0.f, 1.f);
+    float Mr[25];
+#pragma unroll
+    for (int q = 0; q < 25; ++q) Mr[q] = Mh[q];
+    __builtin_amdgcn_wave_barrier();
+    auto geo_at = [&](int row) __attribute__((always_inline)) { return gs[row - grow0]; };
     float ov[WPW][NA];
     // the wave-uniform guards also keep the scheduler from hoisting later walkers' loads (spills)
 #pragma unroll
@@ -2477,17 +2506,17 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       if ((b + ANT) * NA <= rows) {
         float pv[ANT][NA];
 #pragma unroll
-        for (int u = 0; u < ANT; ++u) feat_v<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pv[u]);
-        attn_feat_core<NA, ANT>(Mh, a.feat.geo, b, a.feat.n_up, pv, qs, lane,
-                                reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
+        for (int u = 0; u < ANT; ++u) feat_v_g<NA>(fw, geo_at, b + u, a.feat.n_up, pv[u]);
+        attn_feat_core_g<NA, ANT>(Mr, geo_at, b, a.feat.n_up, pv, qs, lane,
+                                  reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
       } else {  // the batch ends inside this group (last tile)
 #pragma unroll
         for (int u = 0; u < ANT; ++u) {
           if ((b + u + 1) * NA <= rows) {
             float pv[1][NA];
-            feat_v<NA>(fw, a.feat.geo, b + u, a.feat.n_up, pv[0]);
-            attn_feat_core<NA, 1>(Mh, a.feat.geo, b + u, a.feat.n_up, pv, qs, lane,
-                                  reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
+            feat_v_g<NA>(fw, geo_at, b + u, a.feat.n_up, pv[0]);
+            attn_feat_core_g<NA, 1>(Mr, geo_at, b + u, a.feat.n_up, pv, qs, lane,
+                                    reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
           } else {
 #pragma unroll
             for (int i = 0; i < NA; ++i) ov[t + u][i] = 0.f;
@@ -2496,7 +2525,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       }
     }
     if (CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0);
-    __syncthreads();  // the staging areas lie in the planes
+    lbar();  // the staging areas lie in the planes
 #pragma unroll
     for (int t = 0; t < WPW; ++t)
 #pragma unroll
@@ -2511,7 +2540,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
         *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
       }
-    __syncthreads();
+    lbar();
   } else {
     prefetch(a.Wp1, a.ldp1, 0);
     const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
@@ -2520,7 +2549,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       const int r = i / (CH_K / 4), c = 4 * (i % (CH_K / 4));
       put4(r, c, src[i]);
     }
-    __syncthreads();
+    lbar();
   }
   // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
   CHAIN_T(1);
@@ -2608,7 +2637,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
       put4(32 * rb + l32, colof(g), make_float4(x[rb][4 * g], x[rb][4 * g + 1], x[rb][4 * g + 2], x[rb][4 * g + 3]));
-  __syncthreads();
+  lbar();
   // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
   CHAIN_T(5);
   gemm(NoTr{});
@@ -2644,7 +2673,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     }
   }
   if (!a.Wp3) return;
-  __syncthreads();
+  lbar();
   CHAIN_T(9);
   // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
   for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
