@@ -22,6 +22,32 @@
 #include "device_common.h"
 #include "mcmc_common.h"
 
+#ifndef DET_LU_REG  // A/B knob: det_value's LU with one column per lane in registers (1) or eliminate (0)
+#define DET_LU_REG 1
+#endif
+#ifndef DET_GJ_REG  // A/B knob: det_energy_wave's B = Phi0^-1 by register Gauss-Jordan (1) or eliminate (0)
+#define DET_GJ_REG 1
+#endif
+#ifndef DET_STAMP  // diagnostic builds only (tools/det_stamp.py): phase stamps of det_value / det_energy_wave
+#define DET_STAMP 0
+#endif
+#if DET_STAMP
+// [2][DET_STAMP_WG][DET_NSTAMP]: slot 0 = det_value_kernel, slot 1 = det_energy_wave_kernel
+constexpr int DET_STAMP_WG = 1024, DET_NSTAMP = 12;
+__device__ unsigned long long g_det_stamp[2 * DET_STAMP_WG * DET_NSTAMP];
+#define DET_T(slot, i)                                                                                       \
+  do {                                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < DET_STAMP_WG)                                                       \
+      g_det_stamp[((slot) * DET_STAMP_WG + blockIdx.x) * DET_NSTAMP + (i)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+extern "C" int dh_debug_det_stamps(unsigned long long* out, int n) {
+  n = n < 2 * DET_STAMP_WG * DET_NSTAMP ? n : 2 * DET_STAMP_WG * DET_NSTAMP;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_det_stamp), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#else
+#define DET_T(slot, i)
+#endif
+
 namespace dh {
 namespace {
 
@@ -196,6 +222,142 @@ __device__ __forceinline__ void eliminate(cf* A, int lda, int N, int ncol, bool 
   }
 }
 
+// eliminate(Aug, 2N, N, 2N, gj = true) for N <= NMAX, column c of the augmented [A | I] in
+// registers of lane c < 2 N (round 5, det_energy_wave_kernel): the same pivots and log det
+// terms; pivot row scaled by 1 / P, every other row r minus A[r][p] times it.  The factors reach
+// the lanes by shuffles, no LDS round trips.  Not bitwise the LDS form (the compiler fuses the
+// complex products differently); B = A^-1 ends in lanes N .. 2 N - 1.
+template <int NMAX>
+__device__ __forceinline__ cf gj_inverse_cols(cf (&col)[NMAX], int N) {
+  auto is = [](int r, int q) __attribute__((always_inline)) {
+    int m = r == q;
+    asm volatile("" : "+v"(m));
+    return m != 0;
+  };
+  auto pick = [&](int q) __attribute__((always_inline)) {
+    cf v = col[0];
+#pragma unroll
+    for (int r = 1; r < NMAX; ++r)
+      if (is(r, q)) v = col[r];
+    return v;
+  };
+  float lre = 0.f, lim = 0.f;
+  for (int p = 0; p < N; ++p) {
+    float best = -1.f;
+    int bi = N;
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+      if (r >= p && r < N) {
+        const float v = cabs1(col[r]);
+        if (v > best) {
+          best = v;
+          bi = r;
+        }
+      }
+    }
+    int pr = __shfl(bi, p, 64);
+    pr = pr < N ? pr : p;
+    if (pr != p) {
+      const cf a = pick(p), b = pick(pr);
+#pragma unroll
+      for (int r = 0; r < NMAX; ++r) {
+        if (is(r, p)) col[r] = b;
+        if (is(r, pr)) col[r] = a;
+      }
+    }
+    const cf mine = pick(p);
+    const cf P{__shfl(mine.re, p, 64), __shfl(mine.im, p, 64)};
+    const float mag = sqrtf(P.re * P.re + P.im * P.im);
+    lre += logf(mag);
+    lim += atan2f(P.im, P.re) + (pr != p ? kPi : 0.f);
+    const cf rowp = mine * cdiv(cf{1.f, 0.f}, P);
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+      if (r < N) {
+        const cf f{__shfl(col[r].re, p, 64), __shfl(col[r].im, p, 64)};  // A[r][p]
+        cf v = col[r];
+        v.re -= f.re * rowp.re - f.im * rowp.im;
+        v.im -= f.re * rowp.im + f.im * rowp.re;
+        col[r] = is(r, p) ? rowp : v;
+      }
+    }
+  }
+  return cf{lre, lim};
+}
+
+// eliminate(A, N, N, N, gj = false) for N <= NMAX with column c of A in registers of lane c
+// of the (half-)wave (round 5): the same pivots (first maximum of cabs1 at or below the
+// diagonal), the same factors f = A[r][p] / P and updates of columns c >= p, the same log det
+// terms — without LDS round trips or barriers (the pivot search is lane p's own column, the
+// pivot and factors reach the other lanes by shuffles).  Register arrays are indexed only by
+// compile-time constants (selects), or they would go to scratch.
+template <int NMAX>
+__device__ __forceinline__ cf lu_logdet_cols(cf (&col)[NMAX], int N, int lane, int width) {
+  // r == q through an opaque value: left visible, the compiler turns the select chain into a
+  // run-time index of col (and col into scratch)
+  auto is = [](int r, int q) __attribute__((always_inline)) {
+    int m = r == q;
+    asm volatile("" : "+v"(m));
+    return m != 0;
+  };
+  auto pick = [&](int q) __attribute__((always_inline)) {
+    cf v = col[0];
+#pragma unroll
+    for (int r = 1; r < NMAX; ++r)
+      if (is(r, q)) v = col[r];
+    return v;
+  };
+  float lre = 0.f, lim = 0.f;
+  for (int p = 0; p < N; ++p) {
+    float best = -1.f;
+    int bi = N;
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+      if (r >= p && r < N) {
+        const float v = cabs1(col[r]);
+        if (v > best) {
+          best = v;
+          bi = r;
+        }
+      }
+    }
+    int pr = __shfl(bi, p, width);
+    pr = pr < N ? pr : p;
+    if (pr != p) {  // swap rows p and pr (every column)
+      const cf a = pick(p), b = pick(pr);
+#pragma unroll
+      for (int r = 0; r < NMAX; ++r) {
+        if (is(r, p)) col[r] = b;
+        if (is(r, pr)) col[r] = a;
+      }
+    }
+    const cf mine = pick(p);  // A[p][lane]
+    const cf P{__shfl(mine.re, p, width), __shfl(mine.im, p, width)};
+    const float mag = sqrtf(P.re * P.re + P.im * P.im);
+    lre += logf(mag);
+    lim += atan2f(P.im, P.re) + (pr != p ? kPi : 0.f);
+    const cf Pinv = cdiv(cf{1.f, 0.f}, P);
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+      if (r > p && r < N) {
+        // the roundings of eliminate's code (its factor and update as the compiler emits them:
+        // one product of each pair fused), so that equal rows cancel exactly as there and a
+        // singular matrix keeps its zero pivot (psi = 0, tests/test_gpu_grad.py)
+#pragma clang fp contract(off)
+        const cf c = col[r];
+        const cf fl{c.re * Pinv.re - c.im * Pinv.im, __builtin_fmaf(c.im, Pinv.re, c.re * Pinv.im)};
+        const cf f{__shfl(fl.re, p, width), __shfl(fl.im, p, width)};  // lane p's: row r's factor
+        if (lane >= p) {
+          const float tre = __builtin_fmaf(f.re, mine.re, -(f.im * mine.im));
+          const float tim = __builtin_fmaf(f.im, mine.re, f.re * mine.im);
+          col[r] = cf{c.re - tre, c.im - tim};
+        }
+      }
+    }
+  }
+  return cf{lre, lim};
+}
+
 __device__ inline double jastrow_pair(double r, double al, double cst, double* f1, double* f2) {
   const double ar = al + r;
   *f1 = (cst * al * al) / (ar * ar);
@@ -230,6 +392,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
   const int b = live ? bw : nw - 1;  // a dead half repeats the last walker, writes nothing
   const int tid = HW ? (int)(threadIdx.x & 31) : (int)threadIdx.x, nt = HW ? 32 : 64, width = HW ? 32 : 64;
   double* cart = reinterpret_cast<double*>(piv + 2);  // [N][3] unit vectors (double: close pairs)
+  DET_T(0, 0);
   for (int idx = tid; idx < N * M; idx += nt) {
     const int i = idx / M, p = idx % M;
     E0[idx] = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], false, 0.f, true).e0;
@@ -243,6 +406,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
     cart[3 * i + 2] = ct;
   }
   __syncthreads();
+  DET_T(0, 1);
   // Jastrow (blocks.py:76-121): chord distances on the unit sphere, pairs spread over the
   // wave, accumulated in double and reduced with shuffles (one 64-lane wave per walker)
   double Jw = 0.0;
@@ -260,6 +424,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
     }
     for (int o = width >> 1; o > 0; o >>= 1) Jw += __shfl_xor(Jw, o, width);
   }
+  DET_T(0, 2);
   const int G = 64 / N, gj = tid % N, gg = tid / N, NK = N * K, MNK = M * NK;
   for (int k = 0; k < K; ++k) {
     if constexpr (MGV == 0) {  // small rows: one thread per entry, serial over m
@@ -308,9 +473,19 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
       if (gg == 0) A[i * N + gj] = cf{re, im};
     }
     __syncthreads();
-    eliminate(A, N, N, N, false, fac, piv, logdet, tid, nt, width);
-    if (tid == 0) ld[k] = *logdet;
+    DET_T(0, 3);
+    if (N <= 8 && DET_LU_REG) {  // register LU, one column per lane
+      cf col[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) col[r] = (r < N && tid < N) ? A[r * N + tid] : cf{0.f, 0.f};
+      const cf l = lu_logdet_cols<8>(col, N, tid, width);
+      if (tid == 0) ld[k] = l;
+    } else {
+      eliminate(A, N, N, N, false, fac, piv, logdet, tid, nt, width);
+      if (tid == 0) ld[k] = *logdet;
+    }
     __syncthreads();
+    DET_T(0, 4);
   }
   float* lpv = reinterpret_cast<float*>(cart + 3 * N);  // this walker's Re log psi for the epilogue
   if (tid == 0 && live) {
@@ -329,6 +504,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
     logpsi[2 * b + 1] = val_im;
     *lpv = val_re + (float)Jw;
   }
+  DET_T(0, 5);
   if (!epi.on) return;
   // ---- MCMC epilogue (McmcEpi): the accept of epi.step for this walker and its next proposal,
   // lane i < N moving electron i — accept_propose_kernel's arithmetic on the same values
@@ -350,6 +526,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
   }
   if (epi.propose)
     propose_one(th, ph, epi.x2, epi.geo, e, b, tid, N, epi.width, epi.seed, epi.step + 1, epi.woff, epi.noise2);
+  DET_T(0, 6);
 }
 
 // ------------------------------------------------------------------ envelope contraction
@@ -875,7 +1052,7 @@ __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves, b
   L.LB2 = o;
   o += 2 * NN;
   L.asmb = o;  // even offset: doubles
-  o += 2 * (4 * T + 3 * N);
+  o += 2 * (4 * T + 10 * N);
   L.dgeo = o;  // even offset: (sin th, cos th, sin ph, cos ph) in double, from x
   o += 2 * 4 * N;
   L.geo = o;
@@ -948,7 +1125,7 @@ __device__ inline void block_sum4(float v[4], float* red) {
 // arrays, so nothing goes to scratch memory).
 // Shared by det_energy_kernel and det_energy_wave_kernel: ell0 [K], ellt [K T], ellL [K],
 // ellS [3 K] (written by thread 0 / the lanes before the call), geometry geo (f32) / dgeo
-// (f64) / al in LDS, asmb = 2 (4 T + 3 N) floats of LDS scratch; every thread of the
+// (f64) / al in LDS, asmb = 2 (4 T + 10 N) floats of LDS scratch; every thread of the
 // workgroup calls it (one __syncthreads inside), threads tid < T + N do the per-tangent and
 // per-electron parts.
 __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M, int K, float Q, float radius, float lambda,
@@ -965,6 +1142,12 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
   double* Jn = lbi + T;
   double* Jlbn = Jn + N;
   double* pen = Jlbn + N;
+  // per-electron terms of thread 0's sums, formed by threads T + i (their divisions off the
+  // serial thread; thread 0 adds them in the same order, so the sums are unchanged)
+  double* gph = pen + N;     // kappa_i phi_i
+  double* sgi = gph + N;     // [3][N] the gauge terms of S_im
+  double* cotn = sgi + 3 * N;
+  double* mvn = cotn + N;    // [2][N] Q cos ph / sin th, Q sin ph / sin th
   // determinant weights p_k = w_k / Z, w_k = exp(ell0_k - max) (every thread; K is small)
   double lmax = -1e300;
   for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
@@ -1039,6 +1222,21 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
     Jn[i] = J;
     Jlbn[i] = Jlb;
     pen[i] = pe;
+    {
+      const double st = sti, ct = cti, sp = spi, cp = cpi;
+      const double kap = (double)env_gauge(geo[4 * i + 1], M);  // the leaves' kappa
+      gph[i] = kap * (double)x[2 * (b * N + i) + 1];
+      const double cot = ct / st;
+      const double tdot[3] = {-sp, cp, 0.0};
+      const double thp[3] = {cp * cot, sp * cot, -1.0};
+      const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
+      const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) sgi[kk * N + i] = kap * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
+      cotn[i] = cot;
+      mvn[i] = Q * cp / st;
+      mvn[N + i] = Q * sp / st;
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -1087,16 +1285,9 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
     // gauge terms: phase and the flow channels' phi acceleration (see env_flow2)
     double gauge_phase = 0.0;
     for (int i = 0; i < N; ++i) {
-      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
-      const double kap = (double)env_gauge(geo[4 * i + 1], M);  // the leaves' kappa
-      gauge_phase += kap * (double)x[2 * (b * N + i) + 1];
-      const double cot = ct / st;
-      const double tdot[3] = {-sp, cp, 0.0};
-      const double thp[3] = {cp * cot, sp * cot, -1.0};
-      const double dthp_dth[3] = {-cp / (st * st), -sp / (st * st), 0.0};
-      const double dthp_dph[3] = {-sp * cot, cp * cot, 0.0};
+      gauge_phase += gph[i];
 #pragma unroll
-      for (int kk = 0; kk < 3; ++kk) S_im[kk] += kap * (-(dthp_dth[kk] * tdot[kk] - dthp_dph[kk] * thp[kk]));
+      for (int kk = 0; kk < 3; ++kk) S_im[kk] += sgi[kk * N + i];
     }
     pe *= (double)lambda;
     LB_re += Jlb;
@@ -1107,13 +1298,12 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
     }
     double Mv[3] = {0.0, 0.0, 0.0};
     for (int i = 0; i < N; ++i) {
-      const double st = dgeo[4 * i], ct = dgeo[4 * i + 1], sp = dgeo[4 * i + 2], cp = dgeo[4 * i + 3];
-      const double cot = ct / st;
+      const double cot = cotn[i];
       mag_re += (Q * cot) * (Q * cot);
       mag_re += -2.0 * Q * cot * tgi[2 * i + 1];  // 2 i Q cot * t_phi_scaled
       mag_im += 2.0 * Q * cot * tgr[2 * i + 1];
-      Mv[0] += Q * cp / st;
-      Mv[1] += Q * sp / st;
+      Mv[0] += mvn[i];
+      Mv[1] += mvn[N + i];
     }
     const double r2 = (double)radius * radius;
     const double ke_re = (-LB_re - sq_re + mag_re) / (2.0 * r2);
@@ -1466,7 +1656,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
 //      sums are the same FMAs in the same order, the extra terms are added as separate sums.
 // NV: float4 (VEC) or floats per lane per channel row set (N RW floats over 64 lanes).
 struct DetWaveSmem {
-  int S, LS, Fs, leaf, leaf2, Aug, fac, DG, geo, alpha, dgeo, asmb, ell, misc, total;
+  int S, LS, Fs, leaf, leaf2, Aug, fac, DG, geo, alpha, dgeo, asmb, ell, misc, xs, nrm, total;
 };
 __host__ __device__ inline DetWaveSmem det_wave_layout(int N, int M, int K) {
   DetWaveSmem L;
@@ -1499,11 +1689,15 @@ __host__ __device__ inline DetWaveSmem det_wave_layout(int N, int M, int K) {
   L.dgeo = o;
   o += 8 * N;
   L.asmb = o;
-  o += 2 * (4 * T + 3 * N);
+  o += 2 * (4 * T + 10 * N);
   L.ell = o;  // ell0 [K], ellt [K T], ellL [K], ellS [3 K] (complex)
   o += 2 * K * (T + 5);
   L.misc = o;
   o += 8;
+  L.xs = o;  // the walker's (theta, phi) and the harmonics' norms: the leaves read LDS only, so
+  o += 2 * N;  // no global load queues behind the staged channel rows (vmcnt counts in order)
+  L.nrm = o;
+  o += M;
   L.total = o;
   return L;
 }
@@ -1545,6 +1739,8 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
   cf* ellS = ellL + K;
   int* piv = reinterpret_cast<int*>(sm + L.misc);
   cf* logdet = reinterpret_cast<cf*>(sm + L.misc + 2);
+  float* xs = sm + L.xs;
+  float* nrm = sm + L.nrm;
   // lane (i, j): entry (i, j) of every N x N matrix (lanes >= N N carry zeros)
   const bool act = tid < NN;
   const int i = act ? tid / N : 0, j = act ? tid - (tid / N) * N : 0;
@@ -1553,40 +1749,52 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
   // ---- staging: channel c's N rows (own spin block) -> registers -> LDS (row stride S)
   const size_t rowbase = (size_t)b * N * C;
   using PF = typename std::conditional<VEC, float4, float>::type;
-  PF pf[NV];
+  // two channels' rows in flight (DET_WAVE_PF2, round 5): channel c + 2 is requested while c is
+  // contracted, into the buffer c just left
+  // (one buffer for the widest float4 forms, NV >= 8: two would cost the second wave per SIMD)
+  constexpr bool PF2 = !(VEC && NV >= 8);
+  PF pfa[NV], pfb[NV];
   const int unit = VEC ? 4 : 1, RU = RW / unit;  // units per row
-  auto stage_load = [&](int c) __attribute__((always_inline)) {
+  // per unit u: element offsets of its row piece from the walker's first row (channel 0) and
+  // in the staged rows, formed once; a lane without a piece (q >= N RU) re-loads piece 0 and
+  // stores into the Aug area (written afresh after the channel loop), so loads and stores are
+  // unconditional: branches around them made every store wait for all loads (vmcnt(0)), the
+  // other buffer's included
+  const float* Fw = Fp + rowbase * ldF;
+  int goff[NV], soff[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int q = tid + 64 * u;
+    const bool ok = q < N * RU;
+    const int r = ok ? q / RU : 0, w = ok ? q - r * RU : 0;
+    const int blk = (r >= n_up && n_up > 0) ? 1 : 0;
+    goff[u] = r * C * ldF + blk * RW + w * unit;
+    soff[u] = ok ? L.Fs + r * S + w * unit : L.Aug;
+  }
+  auto stage_load = [&](PF (&pf)[NV], int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      const int q = tid + 64 * u;
-      if (q < N * RU) {
-        const int r = q / RU, w = q - r * RU;
-        const int blk = (r >= n_up && n_up > 0) ? 1 : 0;
-        const float* src = Fp + (rowbase + (size_t)r * C + c) * ldF + (size_t)blk * RW + (size_t)w * unit;
-        if constexpr (VEC)
-          pf[u] = *reinterpret_cast<const float4*>(src);
-        else
-          pf[u] = *src;
-      }
+      const float* src = Fw + (goff[u] + c * ldF);
+      if constexpr (VEC)
+        pf[u] = *reinterpret_cast<const float4*>(src);
+      else
+        pf[u] = *src;
     }
   };
-  auto stage_store = [&]() __attribute__((always_inline)) {
+  auto stage_store = [&](const PF (&pf)[NV]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      const int q = tid + 64 * u;
-      if (q < N * RU) {
-        const int r = q / RU, w = q - r * RU;
-        float* dst = Fs + r * S + w * unit;
-        if constexpr (VEC) {
-          reinterpret_cast<float2*>(dst)[0] = make_float2(pf[u].x, pf[u].y);
-          reinterpret_cast<float2*>(dst)[1] = make_float2(pf[u].z, pf[u].w);
-        } else {
-          *dst = pf[u];
-        }
+      float* dst = sm + soff[u];
+      if constexpr (VEC) {
+        reinterpret_cast<float2*>(dst)[0] = make_float2(pf[u].x, pf[u].y);
+        reinterpret_cast<float2*>(dst)[1] = make_float2(pf[u].z, pf[u].w);
+      } else {
+        *dst = pf[u];
       }
     }
   };
 
+  DET_T(1, 0);
   // ---- geometry, flow coefficients (as det_energy_kernel)
   for (int e = tid; e < N; e += 64) {
     const float4 g = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)(b * N + e));
@@ -1601,7 +1809,10 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
     dgeo[4 * e + 1] = ct;
     dgeo[4 * e + 2] = sp;
     dgeo[4 * e + 3] = cp;
+    xs[2 * e] = x[2 * (b * N + e)];
+    xs[2 * e + 1] = x[2 * (b * N + e) + 1];
   }
+  for (int p = tid; p < M; p += 64) nrm[p] = norm[p];
   __syncthreads();
   for (int t = tid; t < T; t += 64) {
     const int e = t >> 1;
@@ -1621,15 +1832,16 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
   const float thh[3] = {gct * gcp, gct * gsp, -gst};
 
   for (int kd = 0; kd < K; ++kd) {
-    stage_load(0);
+    stage_load(pfa, 0);
+    if constexpr (PF2) stage_load(pfb, 1);  // C = 2 N + 5 > 1
     // envelope leaves of every (electron, harmonic): e0, de/dth, de/dph, d2e/dth2 and, for
     // channel 0, LB(e) and the flow second derivatives (same functions as det_energy_kernel)
-    __syncthreads();  // Pt of the previous determinant (aliases leaf2) is consumed
+    lds_barrier();  // Pt of the previous determinant (aliases leaf2) is consumed
     for (int idx = tid; idx < N * M; idx += 64) {
       const int e = idx / M, p = idx - (idx / M) * M;
       const float st = geo[4 * e], ct = geo[4 * e + 1], sp = geo[4 * e + 2], cp = geo[4 * e + 3];
       const float gauge = env_gauge(ct, M);
-      const EnvLeaf lf = env_leaf(x[2 * (b * N + e)], x[2 * (b * N + e) + 1], p, M, norm[p], true, gauge);
+      const EnvLeaf lf = env_leaf(xs[2 * e], xs[2 * e + 1], p, M, nrm[p], true, gauge);
       const float m = (float)p - 0.5f * (float)(M - 1) - gauge;
       float* d = leaf + e * LS + 8 * p;
       reinterpret_cast<float4*>(d)[0] = make_float4(lf.e0.re, lf.e0.im, lf.dth.re, lf.dth.im);
@@ -1641,18 +1853,14 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
       reinterpret_cast<float4*>(d2)[0] = make_float4(lf.lb.re, lf.lb.im, f0.re, f0.im);
       reinterpret_cast<float4*>(d2)[1] = make_float4(f1.re, f1.im, f2.re, f2.im);
     }
+    DET_T(1, 1);
     const float* Frow = Fs + i * S + j * K + kd;  // re at + m NK, im at + MNK + m NK
     const float* lrow = leaf + i * LS;
     const float* l2row = leaf2 + i * LS;
     cf P0{0.f, 0.f}, D0t{0.f, 0.f}, D0p{0.f, 0.f}, L0{0.f, 0.f}, S0[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
     cf Gu[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}}, LB2{0.f, 0.f}, PL{0.f, 0.f};
     cf PS[3] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-    for (int c = 0; c < C; ++c) {
-      lds_barrier();  // the readers of channel c - 1 are done with Fs
-      stage_store();
-      lds_barrier();
-      if (c + 1 < C) stage_load(c + 1);  // in flight while channel c is contracted (and across
-                                         // the next barriers: they wait for LDS only, round 5)
+    auto chan = [&](int c) __attribute__((always_inline)) {
       if (c == 0) {
         for (int m = 0; m < M; ++m) {
           const cf f{Frow[m * NK], Frow[MNK + m * NK]};
@@ -1710,15 +1918,60 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
         else
           PS[2] = Pe + S0[2] + 2.f * Gu[2];
       }
+    };
+    // channel c from buffer c & 1, which then takes channel c + 2 (in flight while c and c + 1
+    // are contracted, and across the barriers: they wait for LDS only).  The loads are
+    // unconditional (past the last channel they re-read it): a load under a branch leaves the
+    // compiler's counted waits at the path without it, and the stores would drain both buffers
+    if constexpr (PF2) {
+      for (int c = 0; c < C; c += 2) {
+        lds_barrier();  // the readers of channel c - 1 are done with Fs
+        stage_store(pfa);
+        lds_barrier();
+        stage_load(pfa, min(c + 2, C - 1));
+        chan(c);
+        if (c + 1 < C) {
+          lds_barrier();
+          stage_store(pfb);
+          lds_barrier();
+        }
+        stage_load(pfb, min(c + 3, C - 1));
+        if (c + 1 < C) chan(c + 1);
+      }
+    } else {
+      for (int c = 0; c < C; ++c) {
+        lds_barrier();
+        stage_store(pfa);
+        lds_barrier();
+        stage_load(pfa, min(c + 1, C - 1));
+        chan(c);
+      }
     }
+    DET_T(1, 2);
     // ---- B = Phi0^-1 (augmented Gauss-Jordan, partial pivoting), log det Phi0
     if (act) {
       Aug[i * 2 * N + j] = P0;
       Aug[i * 2 * N + N + j] = (i == j) ? cf{1.f, 0.f} : cf{0.f, 0.f};
     }
     __syncthreads();
-    eliminate(Aug, 2 * N, N, 2 * N, true, fac, piv, logdet, tid, 64, 64);
-    if (tid == 0) ell0[kd] = *logdet;
+    if (DET_GJ_REG) {  // register Gauss-Jordan, one augmented column per lane
+      cf col[kDetWaveMaxN];
+      const bool lc = tid < 2 * N;
+#pragma unroll
+      for (int r = 0; r < kDetWaveMaxN; ++r)
+        col[r] = (lc && r < N) ? (tid < N ? Aug[r * 2 * N + tid] : cf{r == tid - N ? 1.f : 0.f, 0.f}) : cf{0.f, 0.f};
+      const cf l = gj_inverse_cols<kDetWaveMaxN>(col, N);
+      if (tid >= N && lc)
+#pragma unroll
+        for (int r = 0; r < kDetWaveMaxN; ++r)
+          if (r < N) Aug[r * 2 * N + tid] = col[r];
+      if (tid == 0) ell0[kd] = l;
+      __syncthreads();
+    } else {
+      eliminate(Aug, 2 * N, N, 2 * N, true, fac, piv, logdet, tid, 64, 64);
+      if (tid == 0) ell0[kd] = *logdet;
+    }
+    DET_T(1, 3);
     cf Br[kDetWaveMaxN];
 #pragma unroll
     for (int l = 0; l < kDetWaveMaxN; ++l) Br[l] = (act && l < N) ? Aug[i * 2 * N + N + l] : cf{0.f, 0.f};
@@ -1770,8 +2023,10 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
       for (int k = 0; k < 3; ++k) ellS[3 * kd + k] = cf{v[4 + 4 * k] - v[6 + 4 * k], v[5 + 4 * k] - v[7 + 4 * k]};
     }
   }
+  DET_T(1, 4);
   energy_assembly(tid, N, n_up, M, K, Q, radius, lambda, interaction, b, x, jas, geo, dgeo, al, ell0, ellt, ellL, ellS,
                   reinterpret_cast<double*>(sm + L.asmb), e_l, obs);
+  DET_T(1, 5);
 }
 
 
