@@ -22,8 +22,8 @@
 #include "device_common.h"
 #include "mcmc_common.h"
 
-#ifndef DET_LU_REG  // A/B knob: det_value's LU with one column per lane in registers (1) or eliminate (0)
-#define DET_LU_REG 1
+#ifndef DET_LU_REG  // A/B knob: det_value's LU with one column per lane in registers (1) or eliminate (0):
+#define DET_LU_REG 0  // bitwise equal, measured 0.3-0.7 us per call slower at C2 (profiles/r05_v17_det_ab.txt)
 #endif
 #ifndef DET_GJ_REG  // A/B knob: det_energy_wave's B = Phi0^-1 by register Gauss-Jordan (1) or eliminate (0)
 #define DET_GJ_REG 1
@@ -451,26 +451,53 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
         A[idx] = acc;
       }
     }
-    for (int i = 0; i < (MGV == 0 ? 0 : N); ++i) {
-      const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
-      const float* rp = Fp + ((size_t)b * N + i) * ldF + (size_t)blk * 2 * MNK + (size_t)gj * K + k;
-      float f[2 * (MGV > 0 ? MGV : 1)];
+    if constexpr (MGV > 0) {
+      // row i's F loads in flight while row i - 1 is contracted (two register sets, rows in
+      // pairs; round 5): one row at a time waited for every row's L2 / HBM round trip (C5: 20
+      // rows, 63 % of the kernel, profiles/r05_v17_det_stamps_c5.txt).  The loads are
+      // unconditional (clamped harmonic and row; out-of-range terms zeroed after the load), so
+      // the compiler's counted waits leave the other set in flight.
+      constexpr int NF = 2 * (MGV > 0 ? MGV : 1);
+      auto ldrow = [&](int i, float (&f)[NF]) __attribute__((always_inline)) {
+        const int blk = (i >= n_up && n_up > 0) ? 1 : 0;
+        const float* rp = Fp + ((size_t)b * N + i) * ldF + (size_t)blk * 2 * MNK + (size_t)gj * K + k;
 #pragma unroll
-      for (int u = 0; u < MGV; ++u) {
-        const int m = gg + G * u;
-        const bool ok = gg < G && m < M;
-        f[2 * u] = ok ? rp[(size_t)m * NK] : 0.f;
-        f[2 * u + 1] = ok ? rp[(size_t)MNK + (size_t)m * NK] : 0.f;
-      }
-      cf acc{0.f, 0.f};
+        for (int u = 0; u < MGV; ++u) {
+          const size_t m = (size_t)min(gg + G * u, M - 1);
+          f[2 * u] = rp[m * NK];
+          f[2 * u + 1] = rp[(size_t)MNK + m * NK];
+        }
+      };
+      auto contract = [&](int i, const float (&f)[NF]) __attribute__((always_inline)) {
+        cf acc{0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < MGV; ++u) cfma(acc, cf{f[2 * u], f[2 * u + 1]}, E0[i * M + min(gg + G * u, M - 1)]);
-      float re = acc.re, im = acc.im;
-      for (int q = 1; q < G; ++q) {
-        re += __shfl(acc.re, gj + N * q, 64);
-        im += __shfl(acc.im, gj + N * q, 64);
+        for (int u = 0; u < MGV; ++u) {
+          const int m = gg + G * u;
+          const bool ok = gg < G && m < M;
+          cfma(acc, cf{ok ? f[2 * u] : 0.f, ok ? f[2 * u + 1] : 0.f}, E0[i * M + min(m, M - 1)]);
+        }
+        float re = acc.re, im = acc.im;
+        for (int q = 1; q < G; ++q) {
+          re += __shfl(acc.re, gj + N * q, 64);
+          im += __shfl(acc.im, gj + N * q, 64);
+        }
+        if (gg == 0) A[i * N + gj] = cf{re, im};
+      };
+      float fa[NF], fb[NF];
+      if constexpr (MGV <= 24) {
+        ldrow(0, fa);
+        for (int i = 0; i < N; i += 2) {
+          ldrow(min(i + 1, N - 1), fb);
+          contract(i, fa);
+          ldrow(min(i + 2, N - 1), fa);
+          if (i + 1 < N) contract(i + 1, fb);
+        }
+      } else {  // (the widest forms: a second set would cost the second wave per SIMD)
+        for (int i = 0; i < N; ++i) {
+          ldrow(i, fa);
+          contract(i, fa);
+        }
       }
-      if (gg == 0) A[i * N + gj] = cf{re, im};
     }
     __syncthreads();
     DET_T(0, 3);
@@ -480,7 +507,7 @@ __global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__
       for (int r = 0; r < 8; ++r) col[r] = (r < N && tid < N) ? A[r * N + tid] : cf{0.f, 0.f};
       const cf l = lu_logdet_cols<8>(col, N, tid, width);
       if (tid == 0) ld[k] = l;
-    } else {
+    } else {  // (a 32-row register LU for N = 10, 20 took the C5 form to 256 VGPRs, one wave per SIMD)
       eliminate(A, N, N, N, false, fac, piv, logdet, tid, nt, width);
       if (tid == 0) ld[k] = *logdet;
     }
