@@ -28,6 +28,9 @@
 namespace dh {
 namespace {
 
+#ifndef STATS_ABL  // timing ablations (tools/stats_bench.py only)
+#define STATS_ABL 0
+#endif
 constexpr int kNT = 1024;
 constexpr int kNW = kNT / 64;
 constexpr int kMaxParts = 5;
@@ -71,6 +74,7 @@ struct SelectLds {
   uint32_t hist[kMaxParts * 4][256];
   uint32_t prefix[kMaxParts * 4];
   int kleft[kMaxParts * 4];
+  int src[kMaxParts * 4];  // per pass: the first rank of the part with the same prefix (its histogram)
   int cnt[kMaxParts];
   int wcnt[kNW][kMaxParts];
   float lo[kMaxParts], hi[kMaxParts];  // clip bounds
@@ -134,11 +138,23 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
     const uint32_t hmask = pass == 0 ? 0u : (0xffffffffu << (shift + 8));
+    // ranks of a part whose prefixes agree so far share one histogram (pass 0: all four; later
+    // the two ranks of a quartile, usually): counted once (round 5, half the count work)
+    if (tid < nh) {
+      int sr = tid;
+      for (int r = (tid & ~3); r < tid; ++r)
+        if (L.prefix[r] == L.prefix[tid]) {
+          sr = r;
+          break;
+        }
+      L.src[tid] = sr;
+    }
     for (int j = tid; j < nh * 256; j += kNT) (&L.hist[0][0])[j] = 0u;
     __syncthreads();
     auto count = [&](bool ok, uint32_t u, int p) __attribute__((always_inline)) {
         const uint32_t dig = (u >> shift) & 255u;
         for (int r = 0; r < 4; ++r) {
+          if (L.src[4 * p + r] != 4 * p + r) continue;  // block-uniform
           const bool take = ok && ((u ^ L.prefix[4 * p + r]) & hmask) == 0u;
           // the common case of a wave sharing one digit (leading bits of similar values)
           // becomes one atomic; the rest fall back to per-lane atomics
@@ -172,7 +188,7 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
     __syncthreads();
     // one wave per histogram: find the bin holding rank kleft, descend into it
     for (int hh = w; hh < nh; hh += kNW) {
-      const uint32_t* hb = L.hist[hh];
+      const uint32_t* hb = L.hist[L.src[hh]];
       uint32_t b0 = hb[4 * lane], b1 = hb[4 * lane + 1], b2 = hb[4 * lane + 2], b3 = hb[4 * lane + 3];
       const uint32_t loc = b0 + b1 + b2 + b3;
       uint32_t incl = loc;
@@ -229,6 +245,10 @@ __global__ __launch_bounds__(kNT) void stats_kernel(const float* __restrict__ e_
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   Src src{e_l, obs, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   iqr_bounds(src, B, penalties ? 5 : 2, L);
+#if STATS_ABL & 2  // ablation (timing tools only): quantiles only
+  if (tid == 0) out[0] = L.lo[0] + L.hi[1];
+  return;
+#endif
   double acc[kNQ];
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) acc[q] = 0.0;
