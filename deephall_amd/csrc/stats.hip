@@ -34,7 +34,16 @@ namespace {
 constexpr int kNT = 1024;
 constexpr int kNW = kNT / 64;
 constexpr int kMaxParts = 5;
-constexpr int kCache = 8;  // values per thread held in registers by iqr_bounds (B <= 8192)
+#ifndef STATS_CACHE  // values per thread held in registers by iqr_bounds
+#define STATS_CACHE 4
+#endif
+#ifndef STATS_CPARTS  // parts cached in registers (more, the penalty form: the uncached path)
+#define STATS_CPARTS 2
+#endif
+// (B <= 4096 and the two E_L parts, round 5: with 8 values of all 5 parts the 128-VGPR budget
+// of a 1024-thread workgroup spilled the keys to scratch: 42.8 -> 37.3 us per call at B = 4096;
+// the penalty form, 5 parts, now takes the uncached path: 71 -> 97 us, profiles/r05_v24_stats.txt)
+constexpr int kCache = STATS_CACHE, kCP = STATS_CPARTS;
 
 // order-preserving float -> uint32 (NaN excluded by the caller)
 __device__ __forceinline__ uint32_t fkey(float v) {
@@ -87,19 +96,19 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // the order-preserving keys of this thread's values, read once (B <= kCache * kNT): the
   // passes below then run on registers instead of re-reading global memory between atomics
-  const bool cached = B <= kCache * kNT;
-  uint32_t kc[kCache][kMaxParts];
-  uint64_t okm = 0;  // bit u * kMaxParts + p: value (u, p) is not NaN
+  const bool cached = B <= kCache * kNT && np <= kCP;
+  uint32_t kc[kCache][kCP];
+  uint64_t okm = 0;  // bit u * kCP + p: value (u, p) is not NaN
   if (cached) {
 #pragma unroll
     for (int u = 0; u < kCache; ++u) {
       const int i = tid + u * kNT;
 #pragma unroll
-      for (int p = 0; p < kMaxParts; ++p) {
+      for (int p = 0; p < kCP; ++p) {
         const float v = (p < np && i < B) ? part_value(s, p, i) : NAN;
         const bool ok = !isnan(v);
         kc[u][p] = ok ? fkey(v) : 0u;
-        if (ok) okm |= 1ull << (u * kMaxParts + p);
+        if (ok) okm |= 1ull << (u * kCP + p);
       }
     }
   }
@@ -107,9 +116,10 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
   int c[kMaxParts] = {0, 0, 0, 0, 0};
   if (cached) {
 #pragma unroll
-    for (int u = 0; u < kCache; ++u)
+    for (int u = 0; u < kCache; ++u) {
 #pragma unroll
-      for (int p = 0; p < kMaxParts; ++p) c[p] += (okm >> (u * kMaxParts + p)) & 1ull ? 1 : 0;
+      for (int p = 0; p < kCP; ++p) c[p] += (okm >> (u * kCP + p)) & 1ull ? 1 : 0;
+    }
   } else {
     for (int i = tid; i < B; i += kNT)
       for (int p = 0; p < np; ++p) c[p] += isnan(part_value(s, p, i)) ? 0 : 1;
@@ -172,8 +182,8 @@ __device__ __noinline__ void iqr_bounds(const Src& s, int B, int np, SelectLds& 
       for (int u = 0; u < kCache; ++u) {
         if (u * kNT >= B) break;  // block-uniform
 #pragma unroll
-        for (int p = 0; p < kMaxParts; ++p)
-          if (p < np) count((okm >> (u * kMaxParts + p)) & 1ull, kc[u][p], p);
+        for (int p = 0; p < kCP; ++p)
+          if (p < np) count((okm >> (u * kCP + p)) & 1ull, kc[u][p], p);
       }
     } else {
       for (int i0 = 0; i0 < B; i0 += kNT) {
