@@ -21,8 +21,10 @@ ARCH = os.environ.get("DH_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I", str(ROOT / "include")]
 # per-file extras: the split-bf16 GEMM keeps its f32 subtractions scalar (packed f32 VALU
-# between MFMAs costs more issue cycles than it saves, MI355X_MICROARCH.md cycle table)
-EXTRA = {"gemm_x6.hip": ["-fno-slp-vectorize"]}
+# between MFMAs costs more issue cycles than it saves, MI355X_MICROARCH.md cycle table); the
+# fused channel tail likewise (round 5: the packed form of layer 1's residual spilled 44 B per
+# lane; without it no spills, channel launches 440 -> 438 us, profiles/r05_v26_lnch_noslp_ab.txt)
+EXTRA = {"gemm_x6.hip": ["-fno-slp-vectorize"], "gemm_lnch.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():

@@ -9,7 +9,7 @@ NAME=$1; FLAGS=$2; FILE=${FILE:-gemm_lnch.hip}
 python -c "from deephall_amd import _build; _build.build()" > /dev/null
 mkdir -p ab build/ab
 OBJ=build/ab/$NAME.$FILE.o
-EXTRA=""; [ "$FILE" = "gemm_x6.hip" ] && EXTRA="-fno-slp-vectorize"
+EXTRA=""; { [ "$FILE" = "gemm_x6.hip" ] || [ "$FILE" = "gemm_lnch.hip" ]; } && EXTRA="-fno-slp-vectorize"
 SRC=deephall_amd/csrc/$FILE
 if [ -n "$REV" ]; then SRC=deephall_amd/csrc/_rev_$FILE; git show $REV:deephall_amd/csrc/$FILE > $SRC; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I include $EXTRA $FLAGS \
