@@ -25,6 +25,9 @@
 #ifndef DET_LU_REG  // A/B knob: det_value's LU with one column per lane in registers (1) or eliminate (0):
 #define DET_LU_REG 0  // bitwise equal, measured 0.3-0.7 us per call slower at C2 (profiles/r05_v17_det_ab.txt)
 #endif
+#ifndef DET_WAVE_SQ  // A/B knob: det_energy_wave's envelope leaves with integer powers by squaring (1) or powf (0)
+#define DET_WAVE_SQ 0
+#endif
 #ifndef DET_GJ_REG  // A/B knob: det_energy_wave's B = Phi0^-1 by register Gauss-Jordan (1) or eliminate (0)
 #define DET_GJ_REG 1
 #endif
@@ -102,9 +105,11 @@ __device__ inline EnvLeaf env_leaf(float th, float ph, int p, int M, float norm,
   L.e0 = cf{norm * R * cph, norm * R * sph};
   if (leaves) {
     const float fa = (float)a, fb = (float)b;
-    const float R1 = 0.5f * (fb * ipow(c, a + 1) * ipow(s, b - 1) - fa * ipow(c, a - 1) * ipow(s, b + 1));
-    const float R2 = 0.25f * (fb * (fb - 1.f) * ipow(c, a + 2) * ipow(s, b - 2) - fb * (fa + 1.f) * R -
-                              fa * (fb + 1.f) * R + fa * (fa - 1.f) * ipow(c, a - 2) * ipow(s, b + 2));
+    // sq: the powers by squaring here too (negative exponents 0, as ipow)
+    auto pw = [sq](float x, int e) { return sq ? (e < 0 ? 0.f : ipow_sq(x, e)) : ipow(x, e); };
+    const float R1 = 0.5f * (fb * pw(c, a + 1) * pw(s, b - 1) - fa * pw(c, a - 1) * pw(s, b + 1));
+    const float R2 = 0.25f * (fb * (fb - 1.f) * pw(c, a + 2) * pw(s, b - 2) - fb * (fa + 1.f) * R -
+                              fa * (fb + 1.f) * R + fa * (fa - 1.f) * pw(c, a - 2) * pw(s, b + 2));
     float st, ct;
     sincosf(th, &st, &ct);
     L.dth = cf{norm * R1 * cph, norm * R1 * sph};
@@ -1868,7 +1873,7 @@ __global__ __launch_bounds__(64) DET_WAVE_ATTR void det_energy_wave_kernel(const
       const int e = idx / M, p = idx - (idx / M) * M;
       const float st = geo[4 * e], ct = geo[4 * e + 1], sp = geo[4 * e + 2], cp = geo[4 * e + 3];
       const float gauge = env_gauge(ct, M);
-      const EnvLeaf lf = env_leaf(xs[2 * e], xs[2 * e + 1], p, M, nrm[p], true, gauge);
+      const EnvLeaf lf = env_leaf(xs[2 * e], xs[2 * e + 1], p, M, nrm[p], true, gauge, DET_WAVE_SQ);
       const float m = (float)p - 0.5f * (float)(M - 1) - gauge;
       float* d = leaf + e * LS + 8 * p;
       reinterpret_cast<float4*>(d)[0] = make_float4(lf.e0.re, lf.e0.im, lf.dth.re, lf.dth.im);
