@@ -25,8 +25,8 @@
 #ifndef DET_LU_REG  // A/B knob: det_value's LU with one column per lane in registers (1) or eliminate (0):
 #define DET_LU_REG 0  // bitwise equal, measured 0.3-0.7 us per call slower at C2 (profiles/r05_v17_det_ab.txt)
 #endif
-#ifndef DET_WAVE_SQ  // A/B knob: det_energy_wave's envelope leaves with integer powers by squaring (1) or powf (0)
-#define DET_WAVE_SQ 0
+#ifndef DET_WAVE_SQ  // A/B knob: det_energy_wave's envelope leaves with integer powers by squaring (1) or powf (0):
+#define DET_WAVE_SQ 1  // det_energy 185 -> 170 us at C2, GPU suite green (profiles/r05_v28_det_sq_ab.txt)
 #endif
 #ifndef DET_GJ_REG  // A/B knob: det_energy_wave's B = Phi0^-1 by register Gauss-Jordan (1) or eliminate (0)
 #define DET_GJ_REG 1
