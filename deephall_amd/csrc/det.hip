@@ -1084,7 +1084,7 @@ __host__ __device__ inline DetSmem det_layout(int N, int M, int K, int nwaves, b
   L.LB2 = o;
   o += 2 * NN;
   L.asmb = o;  // even offset: doubles
-  o += 2 * (4 * T + 10 * N);
+  o += 2 * (4 * T + 10 * N + 2 * K);
   L.dgeo = o;  // even offset: (sin th, cos th, sin ph, cos ph) in double, from x
   o += 2 * 4 * N;
   L.geo = o;
@@ -1157,7 +1157,7 @@ __device__ inline void block_sum4(float v[4], float* red) {
 // arrays, so nothing goes to scratch memory).
 // Shared by det_energy_kernel and det_energy_wave_kernel: ell0 [K], ellt [K T], ellL [K],
 // ellS [3 K] (written by thread 0 / the lanes before the call), geometry geo (f32) / dgeo
-// (f64) / al in LDS, asmb = 2 (4 T + 10 N) floats of LDS scratch; every thread of the
+// (f64) / al in LDS, asmb = 2 (4 T + 10 N + 2 K) floats of LDS scratch; every thread of the
 // workgroup calls it (one __syncthreads inside), threads tid < T + N do the per-tangent and
 // per-electron parts.
 __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M, int K, float Q, float radius, float lambda,
@@ -1180,6 +1180,8 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
   double* sgi = gph + N;     // [3][N] the gauge terms of S_im
   double* cotn = sgi + 3 * N;
   double* mvn = cotn + N;    // [2][N] Q cos ph / sin th, Q sin ph / sin th
+  double* pkr = mvn + 2 * N;  // [2][K] the determinant weights p_k for thread 0 (formed once,
+                              // by threads T + N + k: thread 0 used them 4 K times)
   // determinant weights p_k = w_k / Z, w_k = exp(ell0_k - max) (every thread; K is small)
   double lmax = -1e300;
   for (int k = 0; k < K; ++k) lmax = fmax(lmax, (double)ell0[k].re);
@@ -1269,14 +1271,15 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
       mvn[i] = Q * cp / st;
       mvn[N + i] = Q * sp / st;
     }
+  } else {  // (blockDim > 3 N for every launch: 64 or 256 threads, N <= 20)
+    for (int k = tid - T - N; k < K; k += (int)blockDim.x - T - N) pk(k, pkr[k], pkr[K + k]);
   }
   __syncthreads();
   if (tid == 0) {
     const double val_re = 0.5 * log(zz) + lmax, val_im = atan2(zi, zr);
     double LB_re = 0.0, LB_im = 0.0;
     for (int k = 0; k < K; ++k) {
-      double pr, pi_;
-      pk(k, pr, pi_);
+      const double pr = pkr[k], pi_ = pkr[K + k];
       LB_re += pr * ellL[k].re - pi_ * ellL[k].im;
       LB_im += pr * ellL[k].im + pi_ * ellL[k].re;
     }
@@ -1289,8 +1292,7 @@ __device__ __forceinline__ void energy_assembly(int tid, int N, int n_up, int M,
     for (int kk = 0; kk < 3; ++kk) {
       double a_r = 0.0, a_i = 0.0, m1r = 0.0, m1i = 0.0, m2r = 0.0, m2i = 0.0;
       for (int k = 0; k < K; ++k) {
-        double pr, pi_;
-        pk(k, pr, pi_);
+        const double pr = pkr[k], pi_ = pkr[K + k];
         a_r += pr * ellS[3 * k + kk].re - pi_ * ellS[3 * k + kk].im;
         a_i += pr * ellS[3 * k + kk].im + pi_ * ellS[3 * k + kk].re;
         double gur = 0.0, gui = 0.0;
@@ -1721,7 +1723,7 @@ __host__ __device__ inline DetWaveSmem det_wave_layout(int N, int M, int K) {
   L.dgeo = o;
   o += 8 * N;
   L.asmb = o;
-  o += 2 * (4 * T + 10 * N);
+  o += 2 * (4 * T + 10 * N + 2 * K);
   L.ell = o;  // ell0 [K], ellt [K T], ellL [K], ellS [3 K] (complex)
   o += 2 * K * (T + 5);
   L.misc = o;
