@@ -28,6 +28,9 @@
 #ifndef DET_WAVE_SQ  // A/B knob: det_energy_wave's envelope leaves with integer powers by squaring (1) or powf (0):
 #define DET_WAVE_SQ 1  // det_energy 185 -> 170 us at C2, GPU suite green (profiles/r05_v28_det_sq_ab.txt)
 #endif
+#ifndef DET_LEAF_SQ  // A/B knob: the envelope leaves of env_contract / env_stream / det_energy_kernel (N > 8) by powers
+#define DET_LEAF_SQ 1   // by squaring (1) or powf (0): C5 det class 8.41 -> 8.11 ms (profiles/r05_v32_leaf_sq_ab.txt)
+#endif
 #ifndef DET_GJ_REG  // A/B knob: det_energy_wave's B = Phi0^-1 by register Gauss-Jordan (1) or eliminate (0)
 #define DET_GJ_REG 1
 #endif
@@ -733,7 +736,7 @@ __global__ __launch_bounds__(256) void env_contract_kernel(const float* __restri
     for (int r = 0; r < 2; ++r) {
       const int p = lt + r * nlt;
       if (p >= M) break;
-      const EnvLeaf e = env_leaf(th, ph, p, M, nrm[r], true, gauge);
+      const EnvLeaf e = env_leaf(th, ph, p, M, nrm[r], true, gauge, DET_LEAF_SQ);
       wt[p] = e.e0;
       wt[M + p] = e.dth;
       wt[2 * M + p] = e.dph;
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(256, 2) void env_stream_kernel(const float* __restr
     const float thh[3] = {ct * cp, ct * sp, -st};
     if (tid < 10) wt[tid * M1 + M] = cf{0.f, 0.f};
     for (int p = tid; p < M; p += 256) {
-      const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge);
+      const EnvLeaf e = env_leaf(th, ph, p, M, norm[p], true, gauge, DET_LEAF_SQ);
       wt[p] = e.e0;
       wt[M1 + p] = e.dth;
       wt[2 * M1 + p] = e.dph;
@@ -1479,7 +1482,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 8 : 4) void det_energy_kernel(const 
   for (int idx = tid; idx < (PC ? 0 : N * M); idx += nt) {
     const int i = idx / M, p = idx % M;
     const float gauge = env_gauge(geo[4 * i + 1], M);
-    const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true, gauge);
+    const EnvLeaf e = env_leaf(x[2 * (b * N + i)], x[2 * (b * N + i) + 1], p, M, norm[p], true, gauge, DET_LEAF_SQ);
     E0[idx] = e.e0;
     DTH[idx] = e.dth;
     DPH[idx] = e.dph;
