@@ -130,6 +130,8 @@ struct dh_handle {
   float* wt = nullptr;    // transposed GEMM weights for the NT kernels (device)
   uint16_t* wp = nullptr;  // split-bf16 weight planes for the x6 kernels (device)
   float* mqk = nullptr;    // layer 1's per-head score forms (attn_val.h, launch_lowrank_qk)
+  float* ofw = nullptr;    // layer 1's feature-space output map U^T [256 pad][KO] (launch_ofeat_weight)
+  uint16_t* ofp = nullptr;  // its split-bf16 planes [3][x6_plane_rows(D)][KO]
   int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
   bool params_set = false;
@@ -366,6 +368,8 @@ void dh_destroy(dh_handle* h) {
   if (h->wt) (void)hipFree(h->wt);
   if (h->wp) (void)hipFree(h->wp);
   if (h->mqk) (void)hipFree(h->mqk);
+  if (h->ofw) (void)hipFree(h->ofw);
+  if (h->ofp) (void)hipFree(h->ofp);
   if (h->ref) (void)hipFree(h->ref);
   if (h->wb) (void)hipFree(h->wb);
   if (h->wbt) (void)hipFree(h->wbt);
@@ -432,6 +436,17 @@ int derive_weights(dh_handle* h, hipStream_t st) {
     if (!h->mqk) HIP_TRY(hipMalloc(&h->mqk, (size_t)d.H * kMqkStride * sizeof(float)));
     launch_lowrank_qk(d, h->p.W0qkv, h->p.layer[0].bqkv, h->mqk, st);
     h->p.Mqk = h->mqk;
+    // layer 1's attention output in feature space (round 6): o = o~ Wv~, so o Wol = o~ U with
+    // U = Wv~ Wol per head (8 H rows, zero padded to KO); the NT / x6 kernels read U^T
+    const int KO = ofeat_k(d);
+    const size_t nu = (size_t)round_up(d.D, kRowPad) * KO;
+    if (!h->ofw) HIP_TRY(hipMalloc(&h->ofw, nu * sizeof(float)));
+    if (!h->ofp) HIP_TRY(hipMalloc(&h->ofp, (size_t)3 * x6_plane_rows(d.D) * KO * sizeof(uint16_t)));
+    HIP_TRY(hipMemsetAsync(h->ofw, 0, nu * sizeof(float), st));
+    launch_ofeat_weight(d, h->p.W0qkv, h->p.layer[0].bqkv, h->p.layer[0].Wol, h->ofw, st);
+    launch_split_planes(h->ofw, KO, d.D, KO, h->ofp, st);
+    h->p.UT = h->ofw;
+    h->p.UP = h->ofp;
   }
   if (d.D % 32 == 0) {
     // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
@@ -633,14 +648,6 @@ namespace {
 // One Psiformer pass over nw walkers with C channels; leaves orbital features in w.F.
 // geo_ready: w.geo already holds the walkers' geometry (written by the MCMC proposal); the
 // input kernel is then skipped when the geometry is all it would write.
-static bool lnch_feat_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_LNCH_FEAT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false) {
   const Dims& d = h->d;
   const Params& P = h->p;
@@ -671,6 +678,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // the attention kernel when it supports that (fused), else written by the input kernel.
   const bool fold = d.L > 0;
   const bool fused = fold && attention_takes_features(d, C);
+  const int KO = ofeat_k(d);  // layer 1's o~ row length (fused channel attention, chain prologue)
   // log psi, split-bf16: layer 1's residual h = features W0 is formed in the epilogue of
   // its LayerNorm GEMM from geo, so the input kernel only writes the geometry
   const bool h_feat = C == 1 && fused && x6 && ln_fused;
@@ -679,20 +687,16 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // Its 96-row tiles suit up to ~64K walker rows (C2 24576: 256 tiles, C4 40960: 427); at
   // C5 (81920 rows, 2320 orbital columns) the separate GEMMs with 128-row LayerNorm tiles are
   // faster (102.6 vs 103.6 ms per step, tools/chain_bench.py, profiles/)
-  const bool chain = C == 1 && x6 && ln_fused && D == 256 && rows < 65536 && chain_x6_enabled();
-  // local energy, split-bf16, D = 256: the channel layer tail (Wo Wl + LN_ch, Wm + tanh_ch +
-  // LN_ch) and the next linear map in ONE launch per layer (chain_ch_kernel)
-  const bool chain_ch = C > 1 && x6 && nt && D == 256 && chain_ch_supported(d.N);
+  const bool chain = C == 1 && x6 && ln_fused && D == 256 && rows < 65536;
   // local energy, split-bf16, D = 256, N <= 8: GEMM + channel LayerNorm fused per map
-  const bool lnch = C > 1 && x6 && !chain_ch && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&
+  const bool lnch = C > 1 && x6 && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&
                     gemm_lnch_supported(d.N, D);
   // local energy, gemm_lnch: layer 1's residual h0 = f W0 is formed in the first launch's
-  // epilogue from geo (DH_LNCH_FEAT=0 keeps the input kernel writing h0)
-  const bool lnch_feat = lnch && fused && lnch_feat_enabled();  // fused: the input kernel writes no q|k|v
+  // epilogue from geo
+  const bool lnch_feat = lnch && fused;  // fused: the input kernel writes no q|k|v
   // local energy at N = 10, 20 (GEMM + layernorm_ch_quad): the same residual formed by the
   // first LayerNorm launch, the GEMM writing t without it
-  const bool ln_feat = C > 1 && !lnch && !chain_ch && fused && D == 256 && (d.N == 10 || d.N == 20) &&
-                       lnch_feat_enabled();
+  const bool ln_feat = C > 1 && !lnch && fused && D == 256 && (d.N == 10 || d.N == 20);
   {
     const bool wq = fold && !fused;
     if (!(geo_ready && h_feat && !wq)) {
@@ -703,7 +707,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0 && !chain && !chain_ch)
+    if (l > 0 && !chain)
       gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     // log psi, chain form: layer 1's attention runs in the chain kernel's prologue (its o
     // never leaves the CU; attn_val.h)
@@ -713,15 +717,6 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       PROF(PK_ATTN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * (f ? 1.0 : 4.0) * DD);
       launch_attention(d, w.qkv, w.geo, w.o, nw, C, s, f ? P.W0qkv : nullptr, f ? lp.bqkv : nullptr,
                        f ? P.Mqk : nullptr);
-    }
-    if (chain_ch) {
-      const bool last = l + 1 == d.L;
-      const int n3 = last ? d.orb_cols : 3 * D;
-      PROF(PK_GEMM + PK_CH, 2.0 * R * DD * (2.0 * DD + n3), f4 * (3.0 * R * DD + R * n3 + 2.0 * DD * DD + DD * n3));
-      launch_chain_ch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
-                      last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
-                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, w.geo, s);
-      continue;
     }
     if (chain) {
       const bool last = l + 1 == d.L;
@@ -734,10 +729,11 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
         feat.bqkv = lp.bqkv;
         feat.Mqk = P.Mqk;
       }
-      launch_chain_x6(w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2,
-                      last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3), last ? P.borb : P.layer[l + 1].bqkv,
-                      n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows, feat, s,
-                      /*store_h=*/!last);  // the last layer's h is dead: only its orbitals are read
+      // layer 1 with its attention in the prologue: P1 contracts the o~ planes with U (K = 32)
+      launch_chain_x6(w.o, attn_in_chain ? P.UP : lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D),
+                      lp.bm, lp.ln2, last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3),
+                      last ? P.borb : P.layer[l + 1].bqkv, n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows,
+                      feat, s, /*store_h=*/!last);  // the last layer's h is dead: only its orbitals are read
       continue;
     }
     if (ln_fused) {
@@ -763,9 +759,12 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       // channel rows: each linear map and its channel LayerNorm in one launch, in place over h
       // (gemm_lnch.hip; the GEMM output never reaches HBM)
       {
-        PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
-        launch_gemm_lnch(d.N, w.o, lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.geo, w.h, nw * d.N, 0, s,
-                         (lnch_feat && l == 0) ? P.W0 : nullptr, d.n_up);
+        // layer 1 (fused attention): the o~ rows against U, K = ofeat_k
+        const bool of = fused && l == 0;
+        const double KK = of ? KO : DD;
+        PROF(PK_GEMM + PK_CH, 2.0 * R * DD * KK, f4 * (R * KK + 2.0 * R * DD + DD * KK));
+        launch_gemm_lnch(d.N, w.o, of ? P.UP : lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, w.geo, w.h, nw * d.N, 0, s,
+                         (lnch_feat && l == 0) ? P.W0 : nullptr, d.n_up, of ? KO : D);
       }
       {
         PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
@@ -776,7 +775,10 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded);
     // layer 1 with ln_feat: t = o (Wo Wl) + bo Wl, the LayerNorm adds h0 = f W0
     const bool lf = ln_feat && l == 0;
-    gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, lf ? nullptr : w.h, D, w.t, D, D, D);
+    if (fused && l == 0 && C > 1)  // layer 1's o~ rows (attention_feat2_kernel) against U
+      gemm(w.o, KO, nullptr, P.UT, P.UP, KO, lp.bol, lf ? nullptr : w.h, D, w.t, D, D, KO);
+    else
+      gemm(w.o, D, lp.Wol, lp.WolT, lp.WolP, D, lp.bol, lf ? nullptr : w.h, D, w.t, D, D, D);
     {
       PROF(PK_LN + (C > 1 ? PK_CH : 0), 0.0, f4 * R * 2.0 * DD);
       launch_layernorm(d, w.t, nullptr, lp.ln1, w.geo, w.h, nw, C, 0, s, lf ? P.W0 : nullptr);
@@ -787,7 +789,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  if ((!chain && !chain_ch) || d.L == 0)
+  if (!chain || d.L == 0)
     gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
@@ -815,15 +817,6 @@ int value_pass(dh_handle* h, const float* x, int nw, const Work& w, float* logps
     launch_det_value(h->d, w.F, x, h->p.jastrow, h->norm, logpsi, nw, s, epi);
   }
   return check_launch();
-}
-
-// DH_MCMC_FUSE=0 keeps the separate accept / proposal launches (A/B measurements)
-bool mcmc_fuse_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_MCMC_FUSE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 int check_common(dh_handle* h, const void* x, int B, void* ws, size_t ws_bytes, size_t need) {
@@ -864,8 +857,9 @@ int dh_mcmc_step(dh_handle* h, float* x, float* lp, int32_t* n_accept, int B, in
   // proposal's geometry, so the trunk skips its input kernel); the last accept alone
   const bool geo = !h->laughlin;
   // Psiformer: step st's accept and step st + 1's proposal run in the epilogue of step st's
-  // value kernel (McmcEpi, det.hip): one launch fewer per move, bit-identical results
-  const bool fuse = geo && mcmc_fuse_enabled();
+  // value kernel (McmcEpi, det.hip): one launch fewer per move, bit-identical results; the
+  // Laughlin kernel keeps the separate accept / proposal launches
+  const bool fuse = geo;
   for (int st = 0; st < steps; ++st) {
     const float* nz = noise ? noise + st * nstride : nullptr;
     const uint64_t step = counter + (uint64_t)st;

@@ -1108,251 +1108,6 @@ __global__ __launch_bounds__(256) void attention_val_kernel(const float* __restr
 // wave barriers only), the 5-vectors on lanes = (electron, component), then lane = feature
 // column d for o_c,i[d] = o^_c,i . (Wv~[:, d]) and the store: no q|k|v row is ever formed,
 // the 64-wide dots of attention_wave_kernel<N, true> become 30-FMA forms per pair.
-template <int N>
-struct FeatAttnSmem {
-  static constexpr int nn = N * N, T = 2 * N;
-  static constexpr int M = 0, G = 32, F0 = G + 4 * N, FC = F0 + 5 * N, GK = FC + 5 * N, AL = GK + 15 * N,
-                       ACC = AL + 3 * T, OL = ACC + N, OH = OL + 5 * N, A0 = OH + 5 * N, T2 = A0 + nn,
-                       SUB = T2 + nn, AU = SUB + 3 * nn, QK = AU + 3 * nn, S = QK + 3 * nn, P = S + nn,
-                       RM = P + nn, TOTAL = RM + nn;
-};
-
-template <int N>
-__global__ __launch_bounds__(64) void attention_feat_kernel(const float* __restrict__ geo, float* __restrict__ o,
-                                                            int H, const float* __restrict__ W0qkv,
-                                                            const float* __restrict__ bqkv,
-                                                            const float* __restrict__ Mqk, int n_up) {
-  constexpr int dh = 64, T = 2 * N, C = 2 * N + 5, nn = N * N;
-  using L = FeatAttnSmem<N>;
-  extern __shared__ float sm[];
-  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H, lane = threadIdx.x;
-  const int D = H * dh;
-  auto wsync = [] { __builtin_amdgcn_wave_barrier(); };
-  float *Ms = sm + L::M, *g = sm + L::G, *f0 = sm + L::F0, *fc = sm + L::FC, *gk = sm + L::GK, *al = sm + L::AL;
-  float *accS = sm + L::ACC, *oL = sm + L::OL, *oh = sm + L::OH, *A0 = sm + L::A0, *T2 = sm + L::T2;
-  float *SuB = sm + L::SUB, *Au = sm + L::AU, *QK = sm + L::QK, *S = sm + L::S, *P = sm + L::P, *Rm = sm + L::RM;
-  // this lane's output column: Wv~[:, d] = (W0 Wv rows, bv)
-  const int col = h * dh + lane;
-  const float4 wv = make_float4(W0qkv[2 * D + col], W0qkv[3 * D + 2 * D + col], W0qkv[6 * D + 2 * D + col],
-                                W0qkv[9 * D + 2 * D + col]);
-  const float bv = bqkv[2 * D + col];
-  if (lane < 25) Ms[lane] = Mqk[h * kMqkStride + lane];
-  for (int i = lane; i < N; i += 64) {
-    const float4 gi = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + i));  // st ct sp cp
-    g[4 * i] = gi.x;
-    g[4 * i + 1] = gi.y;
-    g[4 * i + 2] = gi.z;
-    g[4 * i + 3] = gi.w;
-    const float4 f = feature_channel<T>(0, i, gi, (i < n_up) ? 1.f : -1.f);
-    f0[5 * i] = f.x;
-    f0[5 * i + 1] = f.y;
-    f0[5 * i + 2] = f.z;
-    f0[5 * i + 3] = f.w;
-    f0[5 * i + 4] = 1.f;
-    accS[i] = 0.f;
-  }
-  for (int q = lane; q < 5 * N; q += 64) oL[q] = 0.f;
-  for (int p = lane; p < nn; p += 64) {
-    T2[p] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) SuB[k * nn + p] = Au[k * nn + p] = 0.f;
-  }
-  wsync();
-  for (int t = lane; t < T; t += 64) {
-    const int i = t >> 1;
-    const float st = g[4 * i], ct = g[4 * i + 1], sp = g[4 * i + 2], cp = g[4 * i + 3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float a;
-      if ((t & 1) == 0)
-        a = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
-      else
-        a = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
-      al[k * T + t] = a;
-    }
-  }
-  for (int q = lane; q < 3 * N; q += 64) {  // g_k,i: alpha-weighted tangent seeds of electron i
-    const int k = q / N, i = q - k * N;
-    const float st = g[4 * i], ct = g[4 * i + 1], sp = g[4 * i + 2], cp = g[4 * i + 3];
-    const float ae = (k == 0) ? -sp : (k == 1 ? cp : 0.f);
-    const float ao = (k == 0) ? -(ct * cp) : (k == 1 ? -(ct * sp) : st);
-    float* d = gk + (k * N + i) * 5;
-    d[0] = -ae * st;
-    d[1] = ae * ct * cp - ao * sp;
-    d[2] = ae * ct * sp + ao * cp;
-    d[3] = 0.f;
-    d[4] = 0.f;
-  }
-  float Mr[25];
-  wsync();
-#pragma unroll
-  for (int q = 0; q < 25; ++q) Mr[q] = Ms[q];
-  // x^T Mqk y of two 5-vectors in LDS
-  auto form = [&](const float* x, const float* y) {
-    float s = 0.f;
-#pragma unroll
-    for (int a = 0; a < 5; ++a) {
-      float u = 0.f;
-#pragma unroll
-      for (int c2 = 0; c2 < 5; ++c2) u = fmaf(Mr[5 * a + c2], y[c2], u);
-      s = fmaf(x[a], u, s);
-    }
-    return s;
-  };
-  // o_c,i[d] for every electron (lane = d) from the 5-vectors oh[i]
-  float* obase = o + (size_t)b * N * C * D + col;
-  auto expand = [&](int c) {
-    wsync();
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const float* u = oh + 5 * i;
-      const float v = fmaf(u[0], wv.x, fmaf(u[1], wv.y, fmaf(u[2], wv.z, fmaf(u[3], wv.w, u[4] * bv))));
-      obase[(size_t)(i * C + c) * D] = v;
-    }
-  };
-  // the current channel's seeds f~_c,i (bias component 0) into fc
-  auto seeds = [&](int c) {
-    for (int i = lane; i < N; i += 64) {
-      const float4 gi = make_float4(g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]);
-      const float4 f = feature_channel<T>(c, i, gi, (i < n_up) ? 1.f : -1.f);
-      fc[5 * i] = f.x;
-      fc[5 * i + 1] = f.y;
-      fc[5 * i + 2] = f.z;
-      fc[5 * i + 3] = f.w;
-      fc[5 * i + 4] = 0.f;
-    }
-  };
-
-  // ---- value channel: A0 = softmax(f~0 Mqk f~0^T), o^_0 = A0 f~0
-  for (int p = lane; p < nn; p += 64) {
-    const int i = p / N, j = p - (p / N) * N;
-    A0[p] = form(f0 + 5 * i, f0 + 5 * j);
-  }
-  wsync();
-  for (int i = lane; i < N; i += 64) {
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < N; ++j) m = fmaxf(m, A0[i * N + j]);
-    float e[N], ssum = 0.f;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      e[j] = expf(A0[i * N + j] - m);
-      ssum += e[j];
-    }
-    const float inv = 1.f / ssum;
-#pragma unroll
-    for (int j = 0; j < N; ++j) A0[i * N + j] = e[j] * inv;
-  }
-  wsync();
-  for (int q = lane; q < 5 * N; q += 64) {
-    const int i = q / 5, a = q - (q / 5) * 5;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < N; ++j) acc = fmaf(A0[i * N + j], f0[5 * j + a], acc);
-    oh[q] = acc;
-  }
-  expand(0);
-
-  // ---- tangents: S_t on row / column e = t / 2 only
-  for (int t = 0; t < T; ++t) {
-    const int c = 1 + t, e = t >> 1;
-    wsync();
-    seeds(c);  // only row e is nonzero
-    wsync();
-    const float* fe = fc + 5 * e;
-    for (int p = lane; p < nn; p += 64) {
-      const int i = p / N, j = p - (p / N) * N;
-      float s = 0.f;
-      if (i == e) s += form(fe, f0 + 5 * j);
-      if (j == e) s += form(f0 + 5 * i, fe);
-      S[p] = s;
-      if (i == e && j == e) accS[e] += 2.f * form(fe, fe);  // s q_t . k_t, twice (S_L)
-    }
-    wsync();
-    for (int p = lane; p < nn; p += 64) {
-      const int i = p / N;
-      float m1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < N; ++j) m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
-      const float sb = S[p] - m1, at = A0[p] * sb;
-      T2[p] = fmaf(sb, sb, T2[p]);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float a = al[k * T + t];
-        SuB[k * nn + p] = fmaf(a, sb, SuB[k * nn + p]);
-        Au[k * nn + p] = fmaf(a, at, Au[k * nn + p]);
-      }
-      Rm[p] = at;
-    }
-    wsync();
-    for (int q = lane; q < 5 * N; q += 64) {
-      const int i = q / 5, a = q - (q / 5) * 5;
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], f0[5 * j + a], acc);
-      acc = fmaf(A0[i * N + e], fe[a], acc);
-      oL[q] = fmaf(2.f * Rm[i * N + e], fe[a], oL[q]);
-      oh[q] = acc;
-    }
-    expand(c);
-  }
-  // ---- flow score terms 2 s qu_k . ku_k = 2 g_k,i^T Mqk g_k,j
-  wsync();
-  for (int p = lane; p < 3 * nn; p += 64) {
-    const int k = p / nn, pp = p - k * nn, i = pp / N, j = pp - (pp / N) * N;
-    QK[p] = 2.f * form(gk + (k * N + i) * 5, gk + (k * N + j) * 5);
-  }
-  // ---- Laplace-Beltrami and flow channels (dense seeds on every electron)
-#pragma unroll 1
-  for (int c = T + 1; c < C; ++c) {
-    const int k = c - T - 2;  // flow axis (k < 0: the Laplace-Beltrami channel)
-    wsync();
-    seeds(c);
-    wsync();
-    for (int p = lane; p < nn; p += 64) {
-      const int i = p / N, j = p - (p / N) * N;
-      float s = form(fc + 5 * i, f0 + 5 * j) + form(f0 + 5 * i, fc + 5 * j);
-      if (k < 0) {
-        if (i == j) s += accS[i];
-        P[p] = T2[p];
-      } else {
-        s += QK[k * nn + p];
-        const float u = SuB[k * nn + p];
-        P[p] = u * u;
-      }
-      S[p] = s;
-    }
-    wsync();
-    for (int p = lane; p < nn; p += 64) {
-      const int i = p / N;
-      float m1 = 0.f, m2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        m1 = fmaf(A0[i * N + j], S[i * N + j], m1);
-        m2 = fmaf(A0[i * N + j], P[i * N + j], m2);
-      }
-      Rm[p] = A0[p] * ((S[p] - m1) + (P[p] - m2));
-    }
-    wsync();
-    for (int q = lane; q < 5 * N; q += 64) {
-      const int i = q / 5, a = q - (q / 5) * 5;
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < N; ++j) acc = fmaf(Rm[i * N + j], f0[5 * j + a], fmaf(A0[i * N + j], fc[5 * j + a], acc));
-      if (k < 0) {
-        acc += oL[q];
-      } else {
-        float a2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < N; ++j) a2 = fmaf(Au[k * nn + i * N + j], gk[(k * N + j) * 5 + a], a2);
-        acc = fmaf(2.f, a2, acc);
-      }
-      oh[q] = acc;
-    }
-    expand(c);
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // attention_feat_kernel restructured (round 5, "feat2"): the same rules in the same feature
 // space, with the tangent channels in O(N) per channel instead of O(N^2) LDS passes and O(N^3)
@@ -1365,6 +1120,9 @@ __global__ __launch_bounds__(64) void attention_feat_kernel(const float* __restr
 // on the pairs each lane owns (p = lane + 64 u), and Au_k = sum_t alpha_kt A_t = A0 * SuB_k is
 // formed once for the flow channels.  The four dense channels (L, S_0..2) keep the pairwise
 // form.  LDS: A0 and three N x N scratch arrays, the rest small (C5: 10 KB per wave).
+// Output (round 6): the 5-vectors o^_c,i themselves (ofeat_k columns per row, dh_internal.h),
+// not o = o^ Wv~: the next map folds Wv~ into its weights (o Wol = o^ U), so each (row, head)
+// writes 8 floats instead of 64.
 template <int N>
 struct Feat2Smem {
   static constexpr int nn = N * N, T = 2 * N;
@@ -1375,9 +1133,7 @@ struct Feat2Smem {
 
 template <int N>
 __global__ __launch_bounds__(64) void attention_feat2_kernel(const float* __restrict__ geo, float* __restrict__ o,
-                                                             int H, const float* __restrict__ W0qkv,
-                                                             const float* __restrict__ bqkv,
-                                                             const float* __restrict__ Mqk, int n_up) {
+                                                             int H, int KO, const float* __restrict__ Mqk, int n_up) {
   constexpr int dh = 64, T = 2 * N, C = 2 * N + 5, nn = N * N;
   constexpr int PP = (nn + 63) / 64, QQ = (5 * N + 63) / 64;  // pairs / (electron, component) per lane
   using L = Feat2Smem<N>;
@@ -1388,10 +1144,6 @@ __global__ __launch_bounds__(64) void attention_feat2_kernel(const float* __rest
   float *g = sm + L::G, *f0 = sm + L::F0, *oh0 = sm + L::OH0, *gk = sm + L::GK, *al = sm + L::AL, *accS = sm + L::ACC;
   float *SR = sm + L::SR, *SC = sm + L::SC, *M1 = sm + L::M1, *M2 = sm + L::M2, *oh = sm + L::OH, *fc = sm + L::FC;
   float *A0 = sm + L::A0, *Ss = sm + L::S, *Ps = sm + L::P, *Rm = sm + L::RM;
-  const int col = h * dh + lane;
-  const float4 wv = make_float4(W0qkv[2 * D + col], W0qkv[3 * D + 2 * D + col], W0qkv[6 * D + 2 * D + col],
-                                W0qkv[9 * D + 2 * D + col]);
-  const float bv = bqkv[2 * D + col];
   float Mr[25];
 #pragma unroll
   for (int q = 0; q < 25; ++q) Mr[q] = Mqk[h * kMqkStride + q];
@@ -1448,14 +1200,19 @@ __global__ __launch_bounds__(64) void attention_feat2_kernel(const float* __rest
     }
     return sres;
   };
-  float* obase = o + (size_t)b * N * C * D + col;
+  // channel c's o~ rows: this head's 8-column segment (the five sums, three zeros) of every
+  // electron, lane = (electron, slot); the last head also zeroes the columns past 8 H
+  float* obase = o + (size_t)b * N * C * KO;
+  const int tail = h == H - 1 ? KO - 8 * H : 0;
   auto expand = [&](int c) __attribute__((always_inline)) {
     wsync();
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const float* u = oh + 5 * i;
-      const float v = fmaf(u[0], wv.x, fmaf(u[1], wv.y, fmaf(u[2], wv.z, fmaf(u[3], wv.w, u[4] * bv))));
-      obase[(size_t)(i * C + c) * D] = v;
+    for (int q = lane; q < 8 * N; q += 64) {
+      const int i = q >> 3, a = q & 7;
+      obase[(size_t)(i * C + c) * KO + 8 * h + a] = a < 5 ? oh[5 * i + a] : 0.f;
+    }
+    for (int q = lane; q < tail * N; q += 64) {
+      const int i = q / tail;
+      obase[(size_t)(i * C + c) * KO + 8 * H + (q - i * tail)] = 0.f;
     }
   };
 
@@ -1670,37 +1427,11 @@ __global__ __launch_bounds__(64) void attention_feat2_kernel(const float* __rest
   }
 }
 
-static bool attn_feat2_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_ATTN_FEAT2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// DH_ATTN_FEAT=0 keeps attention_wave_kernel<N, true> / the MFMA kernel for layer 1's channel
-// attention (A/B measurements)
-static bool attn_feat_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_ATTN_FEAT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int N>
-void launch_feat(const Dims& d, const float* geo, float* o, int nw, const float* W0qkv, const float* bqkv,
-                 const float* Mqk, hipStream_t s) {
-  if (attn_feat2_enabled()) {
-    const size_t smem2 = (size_t)Feat2Smem<N>::TOTAL * sizeof(float);
-    ensure_smem(attention_feat2_kernel<N>, smem2);
-    hipLaunchKernelGGL(attention_feat2_kernel<N>, dim3(nw * d.H), dim3(64), smem2, s, geo, o, d.H, W0qkv, bqkv, Mqk,
-                       d.n_up);
-    return;
-  }
-  const size_t smem = (size_t)FeatAttnSmem<N>::TOTAL * sizeof(float);
-  ensure_smem(attention_feat_kernel<N>, smem);
-  hipLaunchKernelGGL(attention_feat_kernel<N>, dim3(nw * d.H), dim3(64), smem, s, geo, o, d.H, W0qkv, bqkv, Mqk,
+void launch_feat(const Dims& d, const float* geo, float* o, int nw, const float* Mqk, hipStream_t s) {
+  const size_t smem2 = (size_t)Feat2Smem<N>::TOTAL * sizeof(float);
+  ensure_smem(attention_feat2_kernel<N>, smem2);
+  hipLaunchKernelGGL(attention_feat2_kernel<N>, dim3(nw * d.H), dim3(64), smem2, s, geo, o, d.H, ofeat_k(d), Mqk,
                      d.n_up);
 }
 
@@ -1717,6 +1448,23 @@ __global__ void lowrank_qk_kernel(const float* __restrict__ W0qkv, const float* 
     s += q * k;
   }
   Mqk[h * kMqkStride + 5 * a + c] = (float)(0.125 * s);
+}
+
+// U^T[n][8 h + a] = sum_d Wv~[a][h 64 + d] Wol[h 64 + d][n] (a < 5: Wv~ = the folded W0 Wv
+// rows and bv), f64 sums; padding columns stay as the caller's memset left them (zero)
+__global__ void ofeat_weight_kernel(const float* __restrict__ W0qkv, const float* __restrict__ bqkv,
+                                    const float* __restrict__ Wol, int D, int H, int KO, float* __restrict__ UT) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= D * 8 * H) return;
+  const int n = t / (8 * H), k = t - n * (8 * H), h = k >> 3, a = k & 7, ld = 3 * D;
+  if (a >= 5) return;
+  double s = 0.0;
+  for (int e = 0; e < 64; ++e) {
+    const int col = h * 64 + e;
+    const double v = a < 4 ? (double)W0qkv[a * ld + 2 * D + col] : (double)bqkv[2 * D + col];
+    s += v * (double)Wol[(size_t)col * D + n];
+  }
+  UT[(size_t)n * KO + k] = (float)s;
 }
 
 template <int N>
@@ -1765,22 +1513,29 @@ void launch_lowrank_qk(const Dims& d, const float* W0qkv, const float* bqkv, flo
   hipLaunchKernelGGL(lowrank_qk_kernel, dim3((d.H * 25 + 127) / 128), dim3(128), 0, s, W0qkv, bqkv, d.D, d.H, Mqk);
 }
 
+void launch_ofeat_weight(const Dims& d, const float* W0qkv, const float* bqkv, const float* Wol, float* UT,
+                         hipStream_t s) {
+  const int n = d.D * 8 * d.H;
+  hipLaunchKernelGGL(ofeat_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W0qkv, bqkv, Wol, d.D, d.H,
+                     ofeat_k(d), UT);
+}
+
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,
                       const float* W0qkv, const float* bqkv, const float* Mqk) {
   // wave kernels (value and channel) for dh = 64, N <= 8; W0qkv != nullptr selects the
   // fused layer-1 form (q|k|v from the input features), valid only for those kernels.
-  if (C > 1 && W0qkv && Mqk && d.dh == 64 && attn_feat_enabled() && attention_takes_features(d, C)) {
-    switch (d.N) {  // layer 1, feature space (attention_feat_kernel)
-      case 1: launch_feat<1>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 2: launch_feat<2>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 3: launch_feat<3>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 4: launch_feat<4>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 5: launch_feat<5>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 6: launch_feat<6>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 7: launch_feat<7>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 8: launch_feat<8>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      case 10: launch_feat<10>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
-      default: launch_feat<20>(d, geo, o, nw, W0qkv, bqkv, Mqk, s); return;
+  if (C > 1 && W0qkv && Mqk && d.dh == 64 && attention_takes_features(d, C)) {
+    switch (d.N) {  // layer 1, feature space (attention_feat2_kernel): o holds the o~ rows
+      case 1: launch_feat<1>(d, geo, o, nw, Mqk, s); return;
+      case 2: launch_feat<2>(d, geo, o, nw, Mqk, s); return;
+      case 3: launch_feat<3>(d, geo, o, nw, Mqk, s); return;
+      case 4: launch_feat<4>(d, geo, o, nw, Mqk, s); return;
+      case 5: launch_feat<5>(d, geo, o, nw, Mqk, s); return;
+      case 6: launch_feat<6>(d, geo, o, nw, Mqk, s); return;
+      case 7: launch_feat<7>(d, geo, o, nw, Mqk, s); return;
+      case 8: launch_feat<8>(d, geo, o, nw, Mqk, s); return;
+      case 10: launch_feat<10>(d, geo, o, nw, Mqk, s); return;
+      default: launch_feat<20>(d, geo, o, nw, Mqk, s); return;
     }
   }
   if (C > 1 && attention_mfma_supported(d)) {

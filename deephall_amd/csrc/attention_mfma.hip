@@ -454,14 +454,7 @@ void launch_mfma(const Dims& d, const float* qkv, const float* geo, float* o, in
 
 }  // namespace
 
-// DH_ATTN_MFMA=0 keeps the VALU wave kernels (A/B measurements)
-bool attention_mfma_supported(const Dims& d) {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_ATTN_MFMA");
-    return !(e && e[0] == '0');
-  }();
-  return on && d.dh == 64 && (d.N == 10 || d.N == 20);
-}
+bool attention_mfma_supported(const Dims& d) { return d.dh == 64 && (d.N == 10 || d.N == 20); }
 
 void launch_attention_mfma(const Dims& d, const float* qkv, const float* geo, float* o, int nw, hipStream_t s,
                            const float* W0qkv, const float* bqkv) {

@@ -130,9 +130,13 @@ __host__ __device__ constexpr int attn_feat_floats() { return N * N; }
 // column of v per task and electron (feat_qkv); st: NT x attn_feat_floats(N) floats of
 // wave-private LDS; out[t][i] = o of task t, electron i, column d = lane.
 // geo_at(row): the (st, ct, sp cp) float4 of electron row (global memory or a staged copy)
+// The softmax weights of NT walkers b0 .. b0 + NT - 1 of one head (Mh: its 25 Mqk entries,
+// row-major) into st: NT x attn_feat_floats(N) floats of wave-private LDS, A[t][i][j] at
+// t N^2 + i N + j.  geo_at(row): the (st, ct, sp cp) float4 of electron row (global memory
+// or a staged copy)
 template <int N, int NT, class GeoAt>
-__device__ __forceinline__ void attn_feat_core_g(const float (&M)[25], GeoAt geo_at, int b0, int n_up,
-                                                 const float (&pv)[NT][N], float* st, int lane, float (&out)[NT][N]) {
+__device__ __forceinline__ void attn_feat_weights_g(const float (&M)[25], GeoAt geo_at, int b0, int n_up, float* st,
+                                                    int lane) {
   constexpr int nn = N * N, PER = attn_feat_floats<N>();
   auto feat5g = [&](int row, bool up, float (&f)[5]) __attribute__((always_inline)) {
     const float4 g = geo_at(row);  // st ct sp cp
@@ -176,6 +180,15 @@ __device__ __forceinline__ void attn_feat_core_g(const float (&M)[25], GeoAt geo
     for (int j = 0; j < N; ++j) A[j] = e[j] * inv;
   }
   __builtin_amdgcn_wave_barrier();
+}
+
+// NT walkers of one head; pv: this lane's column of v per task and electron (feat_qkv);
+// out[t][i] = o of task t, electron i, column d = lane.
+template <int N, int NT, class GeoAt>
+__device__ __forceinline__ void attn_feat_core_g(const float (&M)[25], GeoAt geo_at, int b0, int n_up,
+                                                 const float (&pv)[NT][N], float* st, int lane, float (&out)[NT][N]) {
+  constexpr int PER = attn_feat_floats<N>();
+  attn_feat_weights_g<N, NT>(M, geo_at, b0, n_up, st, lane);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const float* A = st + t * PER;
@@ -186,6 +199,36 @@ __device__ __forceinline__ void attn_feat_core_g(const float (&M)[25], GeoAt geo
       for (int j = 0; j < N; ++j) acc = fmaf(A[i * N + j], pv[t][j], acc);
       out[t][i] = acc;
     }
+  }
+}
+
+// Layer 1's attention output in feature space (round 6).  v_j = f~_j Wv~ (Wv~ = [W0 Wv; bv],
+// 5 x 64 per head), so o_i = sum_j A_ij v_j = o~_i Wv~ with o~_i = sum_j A_ij f~_j: five
+// numbers per (walker, electron, head) instead of 64, and o Wol = o~ (Wv~ Wol) = o~ U (the
+// chain kernel's first map contracts over 32 instead of 256).  Outputs in the 8-slot per-head
+// segment of an o~ row (dh_internal.h ofeat_k; slots 5..7 zero): value u of lane p = lane +
+// 64 u is task t = p / (8 N), electron i = p / 8 % N, slot a = p % 8 (p < 8 N NT).
+template <int N, int NT>
+__host__ __device__ constexpr int attn_ofeat_regs() { return (8 * N * NT + 63) / 64; }
+template <int N, int NT, class GeoAt>
+__device__ __forceinline__ void attn_ofeat_core_g(const float (&M)[25], GeoAt geo_at, int b0, int n_up, float* st,
+                                                  int lane, float (&out)[attn_ofeat_regs<N, NT>()]) {
+  constexpr int PER = attn_feat_floats<N>();
+  attn_feat_weights_g<N, NT>(M, geo_at, b0, n_up, st, lane);
+#pragma unroll
+  for (int u = 0; u < attn_ofeat_regs<N, NT>(); ++u) {
+    const int p = lane + 64 * u, t = p / (8 * N), i = (p >> 3) % N, a = p & 7;
+    float acc = 0.f;
+    if (p < 8 * N * NT && a < 5) {
+      const float* A = st + t * PER + i * N;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float4 g = geo_at((b0 + t) * N + j);  // st ct sp cp
+        const float f = a == 0 ? g.y : (a == 1 ? g.x * g.w : (a == 2 ? g.x * g.z : (a == 3 ? (j < n_up ? 1.f : -1.f) : 1.f)));
+        acc = fmaf(A[j], f, acc);
+      }
+    }
+    out[u] = acc;
   }
 }
 

@@ -1049,7 +1049,7 @@ size_t env_contract_smem(int N, int M, int MG, bool WU, int K = 1, bool seg = fa
 // segments, every piece of every wave keeping its lane 0, the lane harmonics within MG;
 // returns the pieces per segment (1, 2), or 0
 int env_contract_seg(int N, int M, int K, int MG, int ldF) {
-  if (K != 1 || std::getenv("DH_ENV_SEG0")) return 0;
+  if (K != 1) return 0;
   const int G = 64 / N, MW = (M + 3) / 4, NK = N * K, MNK = M * NK;
   if ((MW + G - 1) / G > MG || (MW * NK) % 4 || MNK % 4 || ldF % 4) return 0;
   const int seg = (MW * NK * 4 + 1023) / 1024;
@@ -2240,15 +2240,6 @@ void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStrea
                      d.interaction);
 }
 
-// DH_DET_HW=0 keeps one walker per wave in det_value (A/B measurements)
-static bool det_value_hw() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_DET_HW");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 void launch_det_value(const Dims& d, const float* F, const float* x, const float* jastrow, const float* norm,
                       float* logpsi, int nw, hipStream_t s, const McmcEpi& epi) {
   // floats per walker region (+1: the epilogue's log psi slot after the f64 unit vectors)
@@ -2258,11 +2249,11 @@ void launch_det_value(const Dims& d, const float* F, const float* x, const float
                        logpsi, d.N, d.n_up, d.M, d.K, nw, per, epi);
   };
   const int mgv = (d.M + 64 / d.N - 1) / (64 / d.N);  // harmonics per lane
-  if (mgv <= 2 && d.N * d.N <= 64 && det_value_hw()) {
+  if (mgv <= 2 && d.N * d.N <= 64) {
     // two walkers per wave (C2, M = 16, N = 6)
     hipLaunchKernelGGL((det_value_kernel<0, true>), dim3((nw + 1) / 2), dim3(64), (size_t)2 * per * sizeof(float), s, F,
                        d.ld_orb, x, jastrow, norm, logpsi, d.N, d.n_up, d.M, d.K, nw, per, epi);
-  } else if (mgv <= 2)  // C2 (M = 16, N = 6): 0.35 ms serial per entry against 0.41 ms lane groups
+  } else if (mgv <= 2)  // serial per entry (C2 at one walker per wave: 0.35 ms against 0.41 ms lane groups)
     go(det_value_kernel<0>);
   else if (mgv <= 4)
     go(det_value_kernel<4>);
@@ -2288,24 +2279,10 @@ void launch_det_bwd(const Dims& d, const float* F, const float* x, const float* 
 }
 
 bool det_precontract(const Dims& d) {
-  static const int mode = [] {  // DH_DET_PC=0 / 1 forces the direct / precontracted form
-    const char* e = std::getenv("DH_DET_PC");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
   const bool fits = 2 * d.K * d.N <= d.D && d.N <= 32 && d.M <= 16 * 4 * (64 / d.N) && d.M <= 128;
-  if (mode >= 0) return fits && mode == 1;
   // the direct kernel stages small channel rows through LDS (C2: 0.64 ms against 0.93 ms
   // precontracted); larger rows (C4: 3.96 -> 1.92 ms, C5: 52 -> 15.5 ms) go through PhiC
   return fits && !(det_staged(d.N, d.M, d.K) && 2 * d.M * d.N * d.K * d.N <= 8 * 256);
-}
-
-// DH_DET_V2=0 keeps det_energy_kernel for the staged (N <= 8) shapes (A/B measurements)
-static bool det_wave_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_DET_V2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 // det_energy_wave_kernel for this shape: the template's per-lane staging width NV, or 0
@@ -2324,7 +2301,7 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic) {
   bool vec = false;
   const int nv = phic ? 0 : det_wave_nv(d, vec);
-  if (nv > 0 && det_wave_enabled()) {
+  if (nv > 0) {
     const size_t bytes = (size_t)det_wave_layout(d.N, d.M, d.K).total * sizeof(float);
     auto go = [&](auto kern) {
       ensure_smem(kern, bytes);
@@ -2351,33 +2328,14 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
     }
     return;
   }
-  // DH_DET_WAVE=1: one wave per walker (measured slower: C2 0.60 -> 1.21 ms per step, C5
-  // 13.0 -> 14.0 ms; the per-walker work, not the barriers, dominates — DESIGN.md §7.1)
-  static const bool wave_mode = [] {
-    const char* e = std::getenv("DH_DET_WAVE");
-    return e && e[0] == '1';
-  }();
-  const int nrw = 2 * d.M * d.N * d.K * d.N;  // floats of one channel's N staged rows
-  const bool one_wave = wave_mode && 3 * d.N <= 64;
-  const int threads = one_wave ? 64 : 256;
-  const DetSmem L = det_layout(d.N, d.M, d.K, threads / 64, phic != nullptr);
+  const DetSmem L = det_layout(d.N, d.M, d.K, 4, phic != nullptr);
   const size_t bytes = (size_t)L.total * sizeof(float);
   auto go = [&](auto kern) {
     ensure_smem(kern, bytes);
-    hipLaunchKernelGGL(kern, dim3(nw), dim3(threads), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N,
-                       d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction, (const float*)phic);
+    hipLaunchKernelGGL(kern, dim3(nw), dim3(256), bytes, s, F, d.ld_orb, x, geo, jastrow, norm, e_l, obs, d.N, d.n_up,
+                       d.M, d.K, d.Q, d.r, d.lambda, d.interaction, (const float*)phic);
   };
-  if (one_wave && !phic && det_staged(d.N, d.M, d.K)) {
-    if (nrw <= 2 * 64)
-      go(det_energy_kernel<2, false, 64>);
-    else if (nrw <= 6 * 64)
-      go(det_energy_kernel<6, false, 64>);
-    else if (nrw <= 18 * 64)
-      go(det_energy_kernel<18, false, 64>);
-    else
-      go(det_energy_kernel<kStageFloats / 64, false, 64>);
-    return;
-  }
+  const int nrw = 2 * d.M * d.N * d.K * d.N;  // floats of one channel's N staged rows
   if (phic) {
     const int G = 64 / d.N;
     const int mgw = (d.M + G - 1) / G;          // harmonics per lane, one wave per electron
@@ -2390,19 +2348,12 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
                          d.K, d.Q);
     };
     // C5 (N = 20, one spin block, K = 1): rows streamed through registers (env_stream_kernel)
-    static const bool stream = [] {
-      const char* e = std::getenv("DH_ENV_STREAM");
-      return !(e && e[0] == '0');
-    }();
     const int mgs = ((d.M + 3) / 4 + (64 / d.N) - 1) / (64 / d.N);  // harmonics per lane, four waves
-    if (stream && d.N == 20 && d.K == 1 && mgs <= 5) {
+    if (d.N == 20 && d.K == 1 && mgs <= 5) {
       const size_t eb = ((size_t)10 * (d.M + 1) * 2 + 4 * (2 * d.N + 5) * d.N * 2 + 512 + 3 * 2 * d.N) * sizeof(float);
       hipLaunchKernelGGL((env_stream_kernel<20, 5, 8>), dim3(nw * d.N), dim3(256), eb, s, F, d.ld_orb, x, geo, norm,
                          phic, d.n_up, d.M);
-      if (one_wave)
-        go(det_energy_kernel<0, true, 64>);
-      else
-        go(det_energy_kernel<0, true>);
+      go(det_energy_kernel<0, true>);
       return;
     }
     if (mgw <= 4) {  // short rows (C4: M = 24, N = 10): a wave per electron
@@ -2434,17 +2385,11 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
         default: env(env_contract_kernel<16>, 16, false); break;
       }
     }
-    if (one_wave)
-      go(det_energy_kernel<0, true, 64>);
-    else
-      go(det_energy_kernel<0, true>);
+    go(det_energy_kernel<0, true>);
   } else if (!det_staged(d.N, d.M, d.K)) {
-    if (one_wave)
-      go(det_energy_kernel<0, false, 64>);
-    else
-      go(det_energy_kernel<0>);
+    go(det_energy_kernel<0>);
   }
-  else if (nrw <= 8 * threads)
+  else if (nrw <= 8 * 256)
     go(det_energy_kernel<8>);
   else
     go(det_energy_kernel<kStageFloats / 256>);

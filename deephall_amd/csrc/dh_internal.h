@@ -47,7 +47,15 @@ struct Params {
   const uint16_t* WorbB;  // backward planes (untransposed Worb [D][ld_orb])
   const float* WorbBT;    // backward exact-f32 copy Worb^T [ld_orb][D]
   const float* Mqk;       // layer 1's score forms Wq~ Wk~^T / 8, [H][kMqkStride] (attn_val.h)
+  // layer 1's output map in feature space (round 6): U^T [n < D, pad 256][k < ofeat_k] with
+  // U[8 h + a][n] = sum_d Wv~[a][h dh + d] Wol[h dh + d][n] (a < 5; a = 5..7 zero), and its planes
+  const float* UT;
+  const uint16_t* UP;
 };
+// Layer 1's attention output in feature space (attention.hip feat2, the chain prologue): per
+// row o~ [ofeat_k] = per head h the five sums o~_h[a] = sum_j A_ij f~_j[a] (f~ = (z, x, y,
+// spin, 1)) at columns 8 h + a, zeros elsewhere, so o = o~_h Wv~ and o Wol = o~ U (K = ofeat_k)
+inline int ofeat_k(const Dims& d) { return (8 * d.H + 31) / 32 * 32; }
 
 // Channel bookkeeping for one pass: C = 1 (log psi only) or 2N+5 (local energy).
 struct Pass {
@@ -123,18 +131,12 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 // DH_LNCH=0 selects the GEMM + layernorm_ch pair instead.
 bool gemm_lnch_supported(int N, int D);
 int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel; returns the previous form
+// K: X's row length and the contraction (mode 0 only; 256, or layer 1's ofeat_k o~ rows with
+// Wp = the planes of U^T); mode 1 contracts over h's 256 features.
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s,
-                      const float* W0f = nullptr, int n_up = 0);
-bool chain_x6_enabled();
+                      const float* W0f = nullptr, int n_up = 0, int K = 256);
 bool chain_attn_supported(int N, int H, int dh);
-// Channel-row (C > 1) layer tail in one launch (gemm_x6.hip chain_ch_kernel; D = 256):
-// h = LN_ch(h + X1 Wol + b1); h = LN_ch(h + tanh_ch(h Wm + b2)); Y3 = h W3 (+ b3) if Wp3.
-bool chain_ch_supported(int N);
-void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
-                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
-                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, const float* geo,
-                     hipStream_t s);
 // Log-psi layer tail in one launch (D = K = 256): h1 = LN1(h + X1 Wol + b1) (feature
 // residual when feat.W0), h = LN2(h1 + tanh(h1 Wm + b2)), then Y3 = h W3 + b3 if Wp3.
 void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
@@ -174,6 +176,9 @@ void launch_attention(const Dims& d, const float* qkv, const float* geo, float* 
 // layer 1's 5 x 5 score forms per head, Mqk[h][a][b] = sum_d Wq~[a][h dh + d] Wk~[b][h dh + d] / 8
 // (Wq~ / Wk~ = the folded W0 Wqkv rows with the bias as row 4; dh = 64; f64 sums)
 void launch_lowrank_qk(const Dims& d, const float* W0qkv, const float* bqkv, float* Mqk, hipStream_t s);
+// U^T [n][ofeat_k] (row stride ofeat_k, rows n < D; f64 sums) from the folded W0 Wqkv, bqkv and Wol
+void launch_ofeat_weight(const Dims& d, const float* W0qkv, const float* bqkv, const float* Wol, float* UT,
+                         hipStream_t s);
 
 // layernorm.hip
 //   mode 0: h = LN_ch(X)           (X may alias h)

@@ -166,8 +166,11 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ ln,
                                                          const float* __restrict__ geo, float* h, int ne,
-                                                         const float* __restrict__ W0f, int n_up) {
-  constexpr int C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, K = LN_D, BK = LN_BK, NK = K / BK;
+                                                         const float* __restrict__ W0f, int n_up, int kx) {
+  // K: the contraction length = X's row length, a multiple of BK (256; MODE 0 of layer 1 from
+  // the o~ rows: ofeat_k, dh_internal.h); a compile-time 256 in MODE 1
+  constexpr int C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, BK = LN_BK;
+  const int K = MODE == 1 ? LN_D : kx, NK = K / BK;
   constexpr int ROWS = EPT * C;                    // activation rows per tile
   constexpr int NT = NWV * 64, CB = D / (16 * NWV);  // threads; 16-column blocks per wave
   constexpr int PLANE = C * EPT * 64;              // bytes of one bf16 plane per step
@@ -211,15 +214,15 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   // ---- activation pieces of this thread: piece i = tid + NT j -> (row i >> 3, quad i & 7)
   // buffer descriptor over the tile's activation rows (tile-uniform base; rows past the last
   // electron are out of range: their loads return 0)
-  const uint32_t tbytes = (uint32_t)rows_valid * D * 4;
-  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X) + row0 * D, (short)0, tbytes, 0x00020000);
+  const uint32_t tbytes = (uint32_t)rows_valid * D * 4, xbytes = (uint32_t)rows_valid * K * 4;
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X) + row0 * K, (short)0, xbytes, 0x00020000);
   int goff[NQ], loff[NQ];
 #pragma unroll
   for (int j = 0; j < NQ; ++j) {
     const int i = tid + NT * j;
     const int r = i >> 3, q = i & 7;
     const int e = r / C, c = r - e * C;
-    goff[j] = i < ROWS * 8 ? (r * D + 4 * q) * 4 : 0x7fffffff;  // bytes from row0 (k step in soffset)
+    goff[j] = i < ROWS * 8 ? (r * K + 4 * q) * 4 : 0x7fffffff;  // bytes from row0 (k step in soffset)
     loff[j] = (c * EPT + e) * 64 + (((q >> 1) ^ lnch_sw(e)) * 16) + (q & 1) * 8;
     if (!(i < ROWS * 8)) loff[j] = -1;
   }
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) load_w(0, cb, wf[cb]);
     split_store(ra, 0);
-    load_a(1, ra);
+    if (NK > 1) load_a(1, ra);
 #pragma unroll 1
     for (int kt = 0; kt < NK; ++kt) {
       lbar();  // planes of step kt complete; step kt - 1's buffer is free
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     load_a(0, ra);
     load_w(0, 0, wf);
     split_store(ra, 0);
-    load_a(1, ra);
+    if (NK > 1) load_a(1, ra);
 #pragma unroll 1
     for (int kt = 0; kt < NK; ++kt) {
       lbar();  // planes of step kt complete; step kt - 1's buffer is free
@@ -803,28 +806,28 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 
 template <int N, int NWV>
 void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
+                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
   const size_t smem = lnch_smem(N);
   const int grid = (ne + LN_EPT - 1) / LN_EPT;
   if (mode == 0 && W0f) {
     ensure_smem(gemm_lnch_kernel<N, 0, NWV, true>, smem);
     hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV, true>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo,
-                       h, ne, W0f, n_up);
+                       h, ne, W0f, n_up, K);
   } else if (mode == 0) {
     ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);
     hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne, W0f, n_up);
+                       ne, W0f, n_up, K);
   } else {
     ensure_smem(gemm_lnch_kernel<N, 1, NWV>, smem);
     hipLaunchKernelGGL((gemm_lnch_kernel<N, 1, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne, nullptr, 0);
+                       ne, nullptr, 0, LN_D);
   }
 }
 
 template <int N>
 void launch_lnch_n(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
-  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up);
+                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
+  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K);
 }
 
 }  // namespace
@@ -836,37 +839,34 @@ extern "C" int dh_debug_lnch_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-// DH_LNCH: 0 = off (GEMM + layernorm_ch), 1 = gemm_lnch_kernel (16-electron tiles, one per CU)
-static int g_lnch_form = -1;  // -1: not read yet (dh_debug_set_lnch_form overrides it)
-static int lnch_form() {
-  if (g_lnch_form < 0) {
-    const char* v = getenv("DH_LNCH");
-    g_lnch_form = (v && v[0] == '0') ? 0 : 1;
-  }
-  return g_lnch_form;
-}
+// 1 = gemm_lnch_kernel (16-electron tiles, one per CU), 0 = the GEMM + layernorm_ch pair
+// (dh_debug_set_lnch_form: tests and tools only)
+static int g_lnch_form = 1;
 
 int set_lnch_form(int f) {
-  const int old = lnch_form();
+  const int old = g_lnch_form;
   if (f >= 0 && f <= 1) g_lnch_form = f;
   return old;
 }
 
 bool gemm_lnch_supported(int N, int D) {
   if (D != LN_D || N < 1) return false;
-  return lnch_form() == 1 && N <= 6;
+  return g_lnch_form == 1 && N <= 6;
 }
 
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                      const float* geo, float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up) {
-  if (mode != 0) W0f = nullptr;
+                      const float* geo, float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
+  if (mode != 0) {
+    W0f = nullptr;
+    K = LN_D;
+  }
   switch (N) {
-    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
-    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
-    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
-    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
-    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
-    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up); return;
+    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
   }
 }
 

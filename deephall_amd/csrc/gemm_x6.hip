@@ -31,7 +31,6 @@
 #include "attn_val.h"
 #include "dh_internal.h"
 #include "device_common.h"
-#include "ln_ch_wave.h"
 
 #ifndef X6M_BIAS1  // A/B knob: gemm_x6m's epilogue bias loads ahead of its stores (1) or between them (0)
 #define X6M_BIAS1 1
@@ -1929,16 +1928,9 @@ __global__ void split_planes_kernel(const float* __restrict__ Wt, int ldw, int n
 //   P1  h1 = LN1(h + o Wol + bol)                (psiformer.py:44-46; Wol = Wo Wl folded)
 //   P2  h2 = LN2(h1 + tanh(h1 Wm + bm))           (psiformer.py:47-48)  -> h (global)
 //   P3  Y3 = h2 W3 + b3   (optional)              the next layer's q|k|v, or the orbitals
-// A 96-row tile (16 walkers at N = 6) of 3 x 4 waves (32 x 64 wave blocks, as the 96-row
-// LayerNorm GEMM) keeps h1 and h2 in LDS: P2 and P3 take their A operand from that tile
-// (no HBM round trip of h1, no re-read of h2, two launches fewer); only the B planes stream
-// through a two-stage LDS-DMA ring.  LDS: tile 96 x 260 f32 (99 840 B) + ring 2 x 30 720 B.
-// The arithmetic (k order, splits, LayerNorm statistics, tanh) is that of the separate
-// kernels, so the results are bitwise the same (tests/test_gpu_kernels.py).
-constexpr int CH_NW = 3, CH_WN = 4, CH_NWT = 12, CH_TN = 2, CH_BM = 96, CH_BN = 256, CH_LS = 260, CH_K = 256;
-constexpr int CH_A = CH_BM * 16 * 4, CH_BP = CH_BN * 16 * 2, CH_STAGE = CH_A + 3 * CH_BP;
-constexpr size_t CH_TILE = (size_t)CH_BM * CH_LS * 4, CH_SMEM = CH_TILE + 2 * CH_STAGE;
-static_assert(CH_SMEM <= 163840, "chain LDS");
+// 96-row tiles; h1 and h2 stay in the CU (chain_x6s_kernel below).
+constexpr int CH_BM = 96, CH_BN = 256, CH_K = 256;
+constexpr int CH_KO = 32;  // layer 1's o~ rows (H = 4 heads x 8 slots, dh_internal.h ofeat_k)
 
 struct ChainArgs {
   const float* X1;  // o [rows][256]
@@ -1953,262 +1945,10 @@ struct ChainArgs {
   int store_h;  // 0: P2's h is not written back (the last layer: only P3's orbitals are consumed)
 };
 
-__global__ __launch_bounds__(768) void chain_x6_kernel(ChainArgs a) {
-  constexpr int TN = CH_TN, NWT = CH_NWT, LS = CH_LS, nk = CH_K / 16;
-  extern __shared__ float4 smem4[];
-  char* smem = reinterpret_cast<char*>(smem4);
-  float* tile = reinterpret_cast<float*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / CH_WN, wn = wid % CH_WN;
-  const int l32 = lane & 31, lh = lane >> 5;
-  int bid = blockIdx.x;
-  {
-    const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
-    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
-  }
-  const int row0 = bid * CH_BM, rows = a.rows;
-  const uint32_t ring0 = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)(smem + CH_TILE));
-  const int m = wm * 32 + l32;
-  // A fragments: ring image (phase 1, swizzled as x6d) or the f32 tile (phases 2, 3)
-  const int aoff0 = m * 64 + (((2 * lh) ^ ((m >> 2) & 3)) * 16);
-  const int aoff1 = m * 64 + (((2 * lh + 1) ^ ((m >> 2) & 3)) * 16);
-  const int boff = CH_A + wn * TN * 1024 + l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) * 16);
-
-  // DMA of k-tile kt into ring buffer buf: (A pieces 0..5 when xa) + 24 B pieces (1 KB each)
-  auto stage = [&](const char* xa, const char* wb, int ldp, int kt, int buf) __attribute__((always_inline)) {
-    const int IA = xa ? CH_A / 1024 : 0, tot = IA + (3 * CH_BP) / 1024;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int j = wid + t * NWT;
-      if (j >= tot) break;  // wave-uniform
-      uint32_t voff, ldst;
-      const char* base;
-      if (j < IA) {  // 16 rows x 64 B of f32 activations
-        const int r = j * 16 + (lane >> 2);
-        const int sl = ((lane & 3) ^ ((r >> 2) & 3)) * 4;
-        voff = (uint32_t)(r * CH_K + sl) * 4u;
-        ldst = j * 1024;
-        base = xa + kt * 64;
-      } else {  // 32 rows x 32 B of the weight planes
-        const int q = (j - IA) * 32 + (lane >> 1);
-        const int p = q / CH_BN, n = q % CH_BN;
-        const int sl = ((lane & 1) ^ ((n >> 3) & 1)) * 8;
-        voff = (uint32_t)(((size_t)p * ldp + n) * CH_K + sl) * 2u;
-        ldst = CH_A + (j - IA) * 1024;
-        base = wb + kt * 32;
-      }
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + (uint32_t)(buf * CH_STAGE) + ldst);
-      unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(voff), "s"(base), "s"(dst)
-                   : "memory");
-    }
-  };
-  // one GEMM pass over K = 256 (two-buffer ring: k-tile kt+1 lands while kt computes)
-  f32x16 acc[TN];
-  auto gemm = [&](const char* xa, const char* wb, int ldp) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    stage(xa, wb, ldp, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) stage(xa, wb, ldp, kt + 1, cur ^ 1);
-      float4 u, v;
-      if (xa) {
-        const char* As = smem + CH_TILE + cur * CH_STAGE;
-        u = *reinterpret_cast<const float4*>(As + aoff0);
-        v = *reinterpret_cast<const float4*>(As + aoff1);
-      } else {
-        const float* tr = tile + m * LS + 16 * kt + 8 * lh;
-        u = *reinterpret_cast<const float4*>(tr);
-        v = *reinterpret_cast<const float4*>(tr + 4);
-      }
-      bf16x8 c0, c1, c2;
-      split3(u, v, c0, c1, c2);
-      const char* Bc = smem + CH_TILE + cur * CH_STAGE + boff;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(Bc + j * 1024);
-        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(Bc + CH_BP + j * 1024);
-        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(Bc + 2 * CH_BP + j * 1024);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc[j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k-tile kt+1 landed
-      __syncthreads();                                  // ... and buffer cur is free
-    }
-  };
-  // acc (MFMA layout: reg e of acc[j] = row m, column 32 (wn TN + j) + 8 (e >> 2) + 4 lh + (e & 3))
-  auto acc_pos = [&](int j, int g) __attribute__((always_inline)) { return m * LS + 32 * (wn * TN + j) + 8 * g + 4 * lh; };
-  auto acc_col = [&](int j, int g) __attribute__((always_inline)) { return 32 * (wn * TN + j) + 8 * g + 4 * lh; };
-  // row LayerNorm of the tile in place: 16 lanes per row, 4 rows per pass (as the LNM
-  // epilogue of gemm_x6d_kernel); optional residual (R rows or feature residual) and bias
-  // added first; optional copy of the result to global rows of Yg
-  const int sub = lane & 15, rq = lane >> 4;
-  constexpr int NP = CH_BM / (4 * NWT);  // 2 passes
-  auto ln_rows = [&](const float* bias, const float* ln, const float* R, bool feat, float* Yg) __attribute__((always_inline)) {
-    float4 rpre[NP][4];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int r = row0 + 4 * (wid + NWT * p) + rq;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        rpre[p][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < rows) {
-          if (feat) {
-            if (k == 0) rpre[p][0] = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);
-          } else if (R) {
-            rpre[p][k] = *reinterpret_cast<const float4*>(R + (size_t)r * CH_BN + 4 * sub + 64 * k);
-          }
-        }
-      }
-    }
-    float4 bv[4], gm[4], bt[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = 4 * sub + 64 * k;
-      bv[k] = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      gm[k] = *reinterpret_cast<const float4*>(ln + c);
-      bt[k] = *reinterpret_cast<const float4*>(ln + CH_BN + c);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int rr = 4 * (wid + NWT * p) + rq;
-      const int r = row0 + rr;
-      float f[4];
-      if (feat) {
-        const float4 g = rpre[p][0];  // st ct sp cp
-        f[0] = g.y;
-        f[1] = g.x * g.w;
-        f[2] = g.x * g.z;
-        f[3] = (r % a.feat.N < a.feat.n_up) ? 1.f : -1.f;
-      }
-      float4 v[4];
-      float sum = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = 4 * sub + 64 * k;
-        float4 t = *reinterpret_cast<const float4*>(tile + rr * LS + c);
-        t.x += bv[k].x;
-        t.y += bv[k].y;
-        t.z += bv[k].z;
-        t.w += bv[k].w;
-        if (r < rows && (feat || R)) {
-          float4 rv;
-          if (feat) {
-            float4 w0[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) w0[q] = *reinterpret_cast<const float4*>(a.feat.W0 + q * CH_BN + c);
-            rv.x = f[0] * w0[0].x + f[1] * w0[1].x + f[2] * w0[2].x + f[3] * w0[3].x;
-            rv.y = f[0] * w0[0].y + f[1] * w0[1].y + f[2] * w0[2].y + f[3] * w0[3].y;
-            rv.z = f[0] * w0[0].z + f[1] * w0[1].z + f[2] * w0[2].z + f[3] * w0[3].z;
-            rv.w = f[0] * w0[0].w + f[1] * w0[1].w + f[2] * w0[2].w + f[3] * w0[3].w;
-          } else {
-            rv = rpre[p][k];
-          }
-          t.x += rv.x;
-          t.y += rv.y;
-          t.z += rv.z;
-          t.w += rv.w;
-        }
-        v[k] = t;
-        sum += (t.x + t.y) + (t.z + t.w);
-      }
-      const float mean = row16_sum(sum) * (1.f / 256.f);
-      float ss = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[k].x -= mean;
-        v[k].y -= mean;
-        v[k].z -= mean;
-        v[k].w -= mean;
-        ss += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
-      }
-      const float var = row16_sum(ss) * (1.f / 256.f);
-      const float rs = __builtin_amdgcn_rsqf(var + 1e-5f);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float4 o;
-        o.x = gm[k].x * (rs * v[k].x) + bt[k].x;
-        o.y = gm[k].y * (rs * v[k].y) + bt[k].y;
-        o.z = gm[k].z * (rs * v[k].z) + bt[k].z;
-        o.w = gm[k].w * (rs * v[k].w) + bt[k].w;
-        *reinterpret_cast<float4*>(tile + rr * LS + 4 * sub + 64 * k) = o;
-        if (Yg && r < rows) *reinterpret_cast<float4*>(Yg + (size_t)r * CH_BN + 4 * sub + 64 * k) = o;
-      }
-    }
-  };
-
-  // ---- P1: h1 = LN1(h + o Wol + bol) into the tile
-  gemm(reinterpret_cast<const char*>(a.X1 + (size_t)row0 * CH_K), reinterpret_cast<const char*>(a.Wp1), a.ldp1);
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<float4*>(tile + acc_pos(j, g)) =
-          make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
-  __syncthreads();
-  ln_rows(a.b1, a.ln1, a.feat.W0 ? nullptr : a.h, a.feat.W0 != nullptr, nullptr);
-  __syncthreads();
-  // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) into the tile and h
-  gemm(nullptr, reinterpret_cast<const char*>(a.Wp2), a.ldp2);  // ends with a barrier: the tile is free
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float4* tp = reinterpret_cast<float4*>(tile + acc_pos(j, g));
-      const float4 bv = *reinterpret_cast<const float4*>(a.b2 + acc_col(j, g));
-      const float4 r = *tp;
-      *tp = make_float4(r.x + tanh_rat(acc[j][4 * g] + bv.x), r.y + tanh_rat(acc[j][4 * g + 1] + bv.y),
-                        r.z + tanh_rat(acc[j][4 * g + 2] + bv.z), r.w + tanh_rat(acc[j][4 * g + 3] + bv.w));
-    }
-  __syncthreads();
-  ln_rows(nullptr, a.ln2, nullptr, false, a.store_h ? a.h : nullptr);
-  if (!a.Wp3) return;
-  __syncthreads();
-  // ---- P3: Y3 = h2 W3 + b3, 256-column tiles, stored from the MFMA layout (16-B pieces)
-  for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
-    gemm(nullptr, reinterpret_cast<const char*>(a.Wp3 + (size_t)col0 * CH_K), a.ldp3);
-    const int r = row0 + m;
-    if (r < rows) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = col0 + acc_col(j, g);
-          float* yr = a.Y3 + (size_t)r * a.ldy3;
-          if (c + 3 < a.n3) {
-            const float4 bv = *reinterpret_cast<const float4*>(a.b3 + c);
-            *reinterpret_cast<float4*>(yr + c) = make_float4(acc[j][4 * g] + bv.x, acc[j][4 * g + 1] + bv.y,
-                                                             acc[j][4 * g + 2] + bv.z, acc[j][4 * g + 3] + bv.w);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (c + e < a.n3) yr[c + e] = acc[j][4 * g + e] + a.b3[c + e];
-          }
-        }
-    }
-  }
-}
-
-
 // ---- chained layer tail, pre-split activations ------------------------------------------------
-// The production form.  As chain_x6_kernel, but every activation element is split into its
-// three bf16 terms ONCE, by the thread that writes it, into LDS planes [3][96][264] (the
-// x6d/x6r forms re-split the A tile in every wave that reads it: 4-8x the VALU work, the
-// largest cost left in the pass, tools/chain_bench.py), and the weight fragments stream
+// Every activation element is split into its three bf16 terms ONCE, by the thread that
+// writes it, into LDS planes [3][96][264] (an LDS-ring form that re-split the A tile in every
+// wave reading it cost 4-8x the VALU work, round 2), and the weight fragments stream
 // from L2 straight into registers PD k-tiles ahead (no LDS ring, no barrier in a pass).
 // 8 waves; wave w owns output columns 32 w .. 32 w + 31 of a 256-column pass and all 96
 // rows (three 32-row MFMA blocks).  The LayerNorms run on the MFMA layout in registers:
@@ -2249,9 +1989,11 @@ __device__ __forceinline__ void split4(const float4& x, uint2& h, uint2& m, uint
 // so their LDS round trips overlap (round 5: the scores from the features through the head's
 // 5 x 5 form Mqk, no q / k rows), staging the weights in LDS that the planes overwrite
 // afterwards, the o values held in registers (48 per lane) until every wave is done.
-template <int ABLS = 0, int NA = 0>  // ABLS (tools only): 1 weight fragments from one k-tile (L1-resident); 2 no P3 stores
+template <int NA = 0>
 __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
-  constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
+  constexpr int RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
+  using K16 = std::integral_constant<int, CH_K / 16>;                     // a 256-deep pass
+  using KP1 = std::integral_constant<int, (NA > 0 ? CH_KO / 16 : CH_K / 16)>;  // P1: o~ (layer 1) or o
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
@@ -2310,17 +2052,20 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   bf16x8 bq[PD][3];
   const uint16_t* wr = nullptr;
   size_t plane = 0;
-  auto prefetch = [&](const uint16_t* Wp, int ldp, int col0) __attribute__((always_inline)) {
-    plane = (size_t)ldp * CH_K;
-    wr = Wp + (size_t)(col0 + 32 * wid + l32) * CH_K + 8 * lh;
+  // nkt_: 16-wide k-tiles of the pass's contraction (16 = 256; layer 1's P1 from the o~ planes: 2)
+  auto prefetch = [&](const uint16_t* Wp, int ldp, int col0, auto nkt_) __attribute__((always_inline)) {
+    constexpr int NKT = decltype(nkt_)::value, KK = 16 * NKT;
+    plane = (size_t)ldp * KK;
+    wr = Wp + (size_t)(col0 + 32 * wid + l32) * KK + 8 * lh;
 #pragma unroll
-    for (int d = 0; d < PD; ++d)
+    for (int d = 0; d < (PD < NKT ? PD : NKT); ++d)
 #pragma unroll
       for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
   };
   // TR: the operands swapped, D[tile row][output column] (P3's store layout, CHAIN_P3T)
-  auto gemm = [&](auto tr_) __attribute__((always_inline)) {
+  auto gemm = [&](auto tr_, auto nkt_) __attribute__((always_inline)) {
     constexpr bool TR = decltype(tr_)::value;
+    constexpr int nk = decltype(nkt_)::value;
     auto mf = [](const bf16x8& w, const bf16x8& x, const f32x16& c) __attribute__((always_inline)) {
       if constexpr (TR)
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w, c, 0, 0, 0);
@@ -2347,7 +2092,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       if (kt + PD < nk) {
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          bq[kt % PD][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + (ABLS ? 0 : 16 * (kt + PD)));
+          bq[kt % PD][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * (kt + PD));
       }
       bf16x8 cn[RB][3];
       if (kt + 1 < nk) lda(kt + 1, cn);
@@ -2473,20 +2218,18 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
 
   // ---- P1 prologue: o rows -> planes (each element split once)
   if constexpr (NA > 0) {
-    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_K == 256, "walker-aligned tiles, 4 heads x 2 wave groups");
+    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_KO == 32, "walker-aligned tiles, 4 heads x 2 wave groups");
     constexpr int WPW = 48 / NA;  // walkers per wave
-    // walkers per attn_val_core call (their LDS round trips overlap): CHAIN_ANT where it divides
-    constexpr int ANT = (CHAIN_ANT == 4 && WPW % 4 == 0) ? 4 : 2, PER = ANT * attn_val_floats<NA>();
-    static_assert(WPW % 2 == 0 && CS_NW * PER * 4 <= 3 * CS_PLANE, "walker pairs, staging in the planes");
-    if (!CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0);
+    // walkers per attn_ofeat_core_g call (their LDS round trips overlap): CHAIN_ANT where it divides
+    constexpr int ANT = (CHAIN_ANT == 4 && WPW % 4 == 0) ? 4 : 2, PER = ANT * attn_feat_floats<NA>();
+    constexpr int NG = WPW / ANT, RG = attn_ofeat_regs<NA, ANT>();
+    static_assert(WPW % ANT == 0, "walker groups");
+    if (!CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0, KP1{});
     float* qs = reinterpret_cast<float*>(smem) + wid * PER;
     const int hd = wid & 3, wl0 = (wid >> 2) * WPW;  // head; first tile walker of this wave
-    FeatW fw;
-    fw.load(a.feat.W0qkv, a.feat.bqkv, CH_K, hd * 64 + lane);
-    const float* Mh = a.feat.Mqk + hd * kMqkStride;  // the head's score form (attn_feat_core)
+    const float* Mh = a.feat.Mqk + hd * kMqkStride;  // the head's score form (attn_feat_weights_g)
     // the geometry of this wave's WPW walkers, staged once in wave-private LDS past the
-    // staging areas (round 5: every attn_feat_core / feat_v call re-read it from global memory,
-    // a dependent round trip per call), and the head's score form in registers once
+    // staging areas, and the head's score form in registers once
     static_assert(WPW * NA <= 64 && CS_NW * (PER + 4 * WPW * NA) * 4 <= 3 * CS_PLANE, "geometry staging");
     float4* gs = reinterpret_cast<float4*>(reinterpret_cast<float*>(smem) + CS_NW * PER) + wid * WPW * NA;
     const int grow0 = row0 + wl0 * NA;  // first electron row of the wave's walkers
@@ -2498,51 +2241,59 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     for (int q = 0; q < 25; ++q) Mr[q] = Mh[q];
     __builtin_amdgcn_wave_barrier();
     auto geo_at = [&](int row) __attribute__((always_inline)) { return gs[row - grow0]; };
-    float ov[WPW][NA];
-    // the wave-uniform guards also keep the scheduler from hoisting later walkers' loads (spills)
+    // layer 1's o~ (attn_val.h attn_ofeat_core_g): 8 slots per (walker, electron) of this head
+    float ov[NG][RG];
 #pragma unroll
-    for (int t = 0; t < WPW; t += ANT) {
-      const int b = row0 / NA + wl0 + t;
+    for (int tg = 0; tg < NG; ++tg) {
+      const int b = row0 / NA + wl0 + tg * ANT;
       if ((b + ANT) * NA <= rows) {
-        float pv[ANT][NA];
+        attn_ofeat_core_g<NA, ANT>(Mr, geo_at, b, a.feat.n_up, qs, lane, ov[tg]);
+      } else {  // the batch ends inside this group (last tile): whole walkers only, zeros past
+        float o1[attn_ofeat_regs<NA, 1>()];
 #pragma unroll
-        for (int u = 0; u < ANT; ++u) feat_v_g<NA>(fw, geo_at, b + u, a.feat.n_up, pv[u]);
-        attn_feat_core_g<NA, ANT>(Mr, geo_at, b, a.feat.n_up, pv, qs, lane,
-                                  reinterpret_cast<float(&)[ANT][NA]>(ov[t]));
-      } else {  // the batch ends inside this group (last tile)
+        for (int u = 0; u < RG; ++u) ov[tg][u] = 0.f;
 #pragma unroll
-        for (int u = 0; u < ANT; ++u) {
-          if ((b + u + 1) * NA <= rows) {
-            float pv[1][NA];
-            feat_v_g<NA>(fw, geo_at, b + u, a.feat.n_up, pv[0]);
-            attn_feat_core_g<NA, 1>(Mr, geo_at, b + u, a.feat.n_up, pv, qs, lane,
-                                    reinterpret_cast<float(&)[1][NA]>(ov[t + u]));
-          } else {
+        for (int w = 0; w < ANT; ++w) {
+          if ((b + w + 1) * NA <= rows) {
+            attn_ofeat_core_g<NA, 1>(Mr, geo_at, b + w, a.feat.n_up, qs, lane, o1);
+            // walker w's values sit at p = 8 NA w + q of the ANT-walker layout
 #pragma unroll
-            for (int i = 0; i < NA; ++i) ov[t + u][i] = 0.f;
+            for (int u = 0; u < RG; ++u) {
+              const int p = lane + 64 * u, q = p - 8 * NA * w;
+              float v = 0.f;
+#pragma unroll
+              for (int u1 = 0; u1 < attn_ofeat_regs<NA, 1>(); ++u1) {
+                const float x1 = __shfl(o1[u1], q & 63, 64);
+                if (q >= 0 && q < 8 * NA && (q >> 6) == u1) v = x1;
+              }
+              if (q >= 0 && q < 8 * NA) ov[tg][u] = v;
+            }
           }
         }
       }
     }
-    if (CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0);
+    if (CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0, KP1{});
     lbar();  // the staging areas lie in the planes
 #pragma unroll
-    for (int t = 0; t < WPW; ++t)
+    for (int tg = 0; tg < NG; ++tg)
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {  // one element: the three bf16 terms of split4
-        const float x = ov[t][i];
-        const uint32_t h2 = pk_bf16(x, 0.f);
-        const float rx = x - lo_f(h2);
-        const uint32_t m2 = pk_bf16(rx, 0.f);
-        const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
-        const int r = (wl0 + t) * NA + i, c = hd * 64 + lane;
-        *reinterpret_cast<uint16_t*>(pl(0, r, c)) = (uint16_t)h2;
-        *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
-        *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
+      for (int u = 0; u < RG; ++u) {  // one element: the three bf16 terms of split4
+        const int p = lane + 64 * u;
+        if (p < 8 * NA * ANT) {
+          const float x = ov[tg][u];
+          const uint32_t h2 = pk_bf16(x, 0.f);
+          const float rx = x - lo_f(h2);
+          const uint32_t m2 = pk_bf16(rx, 0.f);
+          const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
+          const int r = (wl0 + tg * ANT) * NA + (p >> 3), c = 8 * hd + (p & 7);
+          *reinterpret_cast<uint16_t*>(pl(0, r, c)) = (uint16_t)h2;
+          *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
+          *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
+        }
       }
     lbar();
   } else {
-    prefetch(a.Wp1, a.ldp1, 0);
+    prefetch(a.Wp1, a.ldp1, 0, KP1{});
     const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
 #pragma unroll 4
     for (int i = tid; i < CH_BM * (CH_K / 4); i += 512) {
@@ -2553,7 +2304,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
   // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
   CHAIN_T(1);
-  gemm(NoTr{});
+  gemm(NoTr{}, KP1{});
   CHAIN_T(2);
   {
     // every load of this phase issued before the first use, and P2's weight prefetch after
@@ -2576,7 +2327,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         gq[rb] = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
       }
       __builtin_amdgcn_sched_barrier(0);  // the residual loads ahead of the prefetch in vmcnt's queue
-      prefetch(a.Wp2, a.ldp2, 0);
+      prefetch(a.Wp2, a.ldp2, 0, K16{});
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const int r = row0 + 32 * rb + l32;
@@ -2616,7 +2367,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      prefetch(a.Wp2, a.ldp2, 0);
+      prefetch(a.Wp2, a.ldp2, 0, K16{});
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2640,9 +2391,9 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   lbar();
   // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
   CHAIN_T(5);
-  gemm(NoTr{});
+  gemm(NoTr{}, K16{});
   CHAIN_T(6);
-  if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
+  if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0, K16{});
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2678,7 +2429,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
   for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
     if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
-    gemm(std::integral_constant<bool, CHAIN_P3T != 0>{});
+    gemm(std::integral_constant<bool, CHAIN_P3T != 0>{}, K16{});
     if (col0 < 3 * CH_BN) CHAIN_T(10 + 2 * (col0 / CH_BN));
 #if CHAIN_P3T
     {  // D[tile row][column]: reg q of acc[rb] = row 32 rb + (q & 3) + 8 (q >> 2) + 4 lh, column l32.
@@ -2687,13 +2438,12 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       const int c = col0 + 32 * wid + l32;
       const bool cok = c < a.n3;
       const float bv = cok ? a.b3[c] : 0.f;
-      if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
+      if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN, K16{});
       const int nrow = min(CH_BM, rows - row0), ldb = a.ldy3 * 4;
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.Y3 + (size_t)row0 * a.ldy3, (short)0, nrow * ldb, 0x00020000);
       const int vo = cok ? 4 * lh * ldb + 4 * c : 0x7fffffff;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
-        if (ABLS == 2 && acc[rb][0] != 1234.5f) continue;
 #pragma unroll
         for (int q = 0; q < 16; ++q)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[rb][q] + bv), rs, vo,
@@ -2711,11 +2461,11 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       const int c = col0 + colof(g);
       b3v[g] = CHAIN_P3B && c + 3 < a.n3 ? *reinterpret_cast<const float4*>(a.b3 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
+    if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN, K16{});
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       const int r = row0 + 32 * rb + l32;
-      if (r >= rows || (ABLS == 2 && acc[rb][0] != 1234.5f)) continue;
+      if (r >= rows) continue;
       float* yr = a.Y3 + (size_t)r * a.ldy3;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -2735,249 +2485,6 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
 }
 
-
-// ---- chained channel layer tail ----------------------------------------------------------------
-// The local energy's (2N+5)-channel rows (C > 1) through one layer tail per launch:
-//   P1  h1 = LN_ch(h + o Wol + bol)             (layernorm.hip mode 0)  -> h (in place)
-//   P2  h  = LN_ch(h1 + tanh_ch(h1 Wm + bm))     (mode 1)                -> h
-//   P3  Y3 = h W3 (+ b3 on value rows)           the next layer's q|k|v, or the orbitals
-// as chain_x6s_kernel (activations as LDS bf16 planes split once, weights streamed L2 ->
-// registers, 8 waves of 32 columns x 96 rows), with tiles of E = 96 / C WHOLE electrons
-// (RV = E C rows; C2: 5 electrons = 85 of the 96 MFMA rows), so every electron's channel
-// rows are in one tile: after each GEMM pass the tile goes to an f32 scratch over the
-// planes and one wave per electron runs layernorm.hip's wave algebra (ln_ch_wave) on it.
-// The t / z intermediates never reach HBM; h1 round-trips through h (the mode-1 residual).
-template <int N>
-__global__ __launch_bounds__(512) void chain_ch_kernel(ChainArgs a) {
-  constexpr int ABLS = 0, C = 2 * N + 5, E = CH_BM / C, RV = E * C, LSF = CH_LS;
-  constexpr int nk = CH_K / 16, RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
-  extern __shared__ float4 smem4[];
-  char* smem = reinterpret_cast<char*>(smem4);
-  float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, lh = lane >> 5;
-  int bid = blockIdx.x;
-  {
-    const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
-    bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
-  }
-  const int row0 = bid * RV, rows = a.rows;  // tiles of E whole electrons (RV rows)
-  // plane p, tile row r, column c (bf16 units)
-  auto pl = [&](int p, int r, int c) __attribute__((always_inline)) {
-    return smem + (size_t)p * CS_PLANE + (size_t)r * (LSP * 2) + c * 2;
-  };
-  // write 4 consecutive f32 of row r, columns c..c+3 as their three bf16 terms
-  auto put4 = [&](int r, int c, const float4& x) __attribute__((always_inline)) {
-    uint2 h, m, l;
-    split4(x, h, m, l);
-    *reinterpret_cast<uint2*>(pl(0, r, c)) = h;
-    *reinterpret_cast<uint2*>(pl(1, r, c)) = m;
-    *reinterpret_cast<uint2*>(pl(2, r, c)) = l;
-  };
-  // the f32 value back from the planes (exact: a = a0 + a1 + a2 with no rounding)
-  auto get4 = [&](int r, int c) __attribute__((always_inline)) {
-    const uint2 h = *reinterpret_cast<const uint2*>(pl(0, r, c));
-    const uint2 m = *reinterpret_cast<const uint2*>(pl(1, r, c));
-    const uint2 l = *reinterpret_cast<const uint2*>(pl(2, r, c));
-    return make_float4((lo_f(h.x) + lo_f(m.x)) + lo_f(l.x), (hi_f(h.x) + hi_f(m.x)) + hi_f(l.x),
-                       (lo_f(h.y) + lo_f(m.y)) + lo_f(l.y), (hi_f(h.y) + hi_f(m.y)) + hi_f(l.y));
-  };
-
-  // ---- one GEMM pass: acc[rb] = rows 32 rb + l32 x columns col0 + 32 wid + ..  The weight
-  // fragments of its first PD k-tiles are requested by prefetch() beforehand, ahead of the
-  // previous pass's epilogue: its stores then do not sit in front of them in vmcnt's queue
-  f32x16 acc[RB];
-  bf16x8 bq[PD][3];
-  const uint16_t* wr = nullptr;
-  size_t plane = 0;
-  auto prefetch = [&](const uint16_t* Wp, int ldp, int col0) __attribute__((always_inline)) {
-    plane = (size_t)ldp * CH_K;
-    wr = Wp + (size_t)(col0 + 32 * wid + l32) * CH_K + 8 * lh;
-#pragma unroll
-    for (int d = 0; d < PD; ++d)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
-  };
-  auto gemm = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[rb][e] = 0.f;
-    // A fragments of k-tile kt (rows 32 rb + l32, k = 16 kt + 8 lh ..), read one k-tile ahead
-    bf16x8 ca[RB][3];
-    auto lda = [&](int kt, bf16x8(&d)[RB][3]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          d[rb][p] = *reinterpret_cast<const bf16x8*>(pl(p, 32 * rb + l32, 16 * kt + 8 * lh));
-    };
-    lda(0, ca);
-#pragma unroll
-    for (int kt = 0; kt < nk; ++kt) {
-      const bf16x8 b0 = bq[kt % PD][0], b1 = bq[kt % PD][1], b2 = bq[kt % PD][2];
-      if (kt + PD < nk) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bq[kt % PD][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + (ABLS ? 0 : 16 * (kt + PD)));
-      }
-      bf16x8 cn[RB][3];
-      if (kt + 1 < nk) lda(kt + 1, cn);
-      // keep the prefetches where they are: the scheduler would sink each load to just
-      // before its first use and expose the L2 / LDS latency
-      __builtin_amdgcn_sched_barrier(0);
-      // product-major over the three row blocks: consecutive MFMAs are independent
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][2], acc[rb], 0, 0, 0);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, ca[rb][0], acc[rb], 0, 0, 0);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][1], acc[rb], 0, 0, 0);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][1], acc[rb], 0, 0, 0);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, ca[rb][0], acc[rb], 0, 0, 0);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, ca[rb][0], acc[rb], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nk) {
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) ca[rb][p] = cn[rb][p];
-      }
-    }
-  };
-  // MFMA layout: reg 4 g + e of acc[rb] = tile row 32 rb + l32, column 32 wid + 8 g + 4 lh + e
-  auto colof = [&](int g) __attribute__((always_inline)) { return 32 * wid + 8 * g + 4 * lh; };
-  float* scr = reinterpret_cast<float*>(smem);  // [96][LSF] f32 scratch over the planes
-  // acc (+ bias on the value-channel rows, + residual R) -> scratch, MFMA layout
-  auto acc_to_scr = [&](const float* bias, const float* R) __attribute__((always_inline)) {
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int r = 32 * rb + l32, rg = row0 + r;
-      const bool val = (r % C) == 0, own = r < RV && rg < rows;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float4 v = make_float4(acc[rb][4 * g], acc[rb][4 * g + 1], acc[rb][4 * g + 2], acc[rb][4 * g + 3]);
-        if (val) {
-          const float4 bv = *reinterpret_cast<const float4*>(bias + colof(g));
-          v.x += bv.x;
-          v.y += bv.y;
-          v.z += bv.z;
-          v.w += bv.w;
-        }
-        if (R && own) {
-          const float4 rv = *reinterpret_cast<const float4*>(R + (size_t)rg * CH_BN + colof(g));
-          v.x += rv.x;
-          v.y += rv.y;
-          v.z += rv.z;
-          v.w += rv.w;
-        }
-        *reinterpret_cast<float4*>(scr + r * LSF + colof(g)) = v;
-      }
-    }
-  };
-  // scratch (f32) -> planes, in place: every thread holds its 12 float4 across the barrier
-  auto scr_to_planes = [&]() __attribute__((always_inline)) {
-    float4 v[CH_BM * (CH_BN / 4) / 512];
-#pragma unroll
-    for (int i = 0; i < CH_BM * (CH_BN / 4) / 512; ++i) {
-      const int q = tid + 512 * i, r = q / (CH_BN / 4), c = 4 * (q % (CH_BN / 4));
-      v[i] = *reinterpret_cast<const float4*>(scr + r * LSF + c);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < CH_BM * (CH_BN / 4) / 512; ++i) {
-      const int q = tid + 512 * i, r = q / (CH_BN / 4), c = 4 * (q % (CH_BN / 4));
-      put4(r, c, v[i]);
-    }
-    __syncthreads();
-  };
-  const int eg = row0 / C + wid;                       // this wave's electron (LayerNorm stage)
-  const bool lnw = wid < E && (eg + 1) * C <= rows;   // wave-uniform
-  const int sub4 = 4 * lane;
-  auto srow = [&](int c) __attribute__((always_inline)) {
-    return reinterpret_cast<float4*>(scr + (wid * C + c) * LSF + sub4);
-  };
-  auto grow = [&](int c) __attribute__((always_inline)) {
-    return reinterpret_cast<float4*>(a.h + ((size_t)eg * C + c) * CH_BN + sub4);
-  };
-
-  // ---- P1 prologue: o rows -> planes (each element split once)
-  prefetch(a.Wp1, a.ldp1, 0);
-  {
-    const float4* src = reinterpret_cast<const float4*>(a.X1 + (size_t)row0 * CH_K);
-#pragma unroll 4
-    for (int i = tid; i < CH_BM * (CH_K / 4); i += 512) {
-      const int r = i / (CH_K / 4), c = 4 * (i % (CH_K / 4));
-      put4(r, c, src[i]);
-    }
-    __syncthreads();
-  }
-  // ---- P1: h1 = LN_ch(o Wol + bol + h) -> h (global, in place) and the planes
-  gemm();
-  __syncthreads();  // every wave is past its GEMM reads of the planes
-  acc_to_scr(a.b1, a.h);
-  __syncthreads();
-  if (lnw)
-    ln_ch_wave<N>(
-        0, [&](int c) { return *srow(c); }, [&](int c) { return *srow(c); },
-        [&](int c, const float4& v) {
-          *srow(c) = v;
-          *grow(c) = v;
-        },
-        a.ln1, a.feat.geo, eg / N, lane);
-  __syncthreads();
-  // (the next pass's weights are requested here, not before the epilogue: held across the
-  // LayerNorm and the plane conversion they push the kernel past 256 VGPRs)
-  prefetch(a.Wp2, a.ldp2, 0);
-  scr_to_planes();
-  // ---- P2: h2 = LN_ch(h1 + tanh_ch(h1 Wm + bm)) -> h (and the planes for P3)
-  gemm();
-  __syncthreads();
-  acc_to_scr(a.b2, nullptr);
-  __syncthreads();
-  if (lnw)
-    ln_ch_wave<N>(
-        1, [&](int c) { return *srow(c); }, [&](int c) { return *grow(c); },
-        [&](int c, const float4& v) {
-          *grow(c) = v;
-          *srow(c) = v;
-        },
-        a.ln2, a.feat.geo, eg / N, lane);
-  if (!a.Wp3) return;
-  __syncthreads();
-  if (32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0);
-  scr_to_planes();
-  // ---- P3: Y3 = h2 W3 (+ b3 on the value rows), 256-column passes, MFMA-layout stores
-  for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
-    if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
-    gemm();
-    if (col0 + CH_BN + 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, col0 + CH_BN);
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int r = 32 * rb + l32, rg = row0 + r;
-      if (r >= RV || rg >= rows) continue;
-      const bool val = (r % C) == 0;
-      float* yr = a.Y3 + (size_t)rg * a.ldy3;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = col0 + colof(g);
-        if (c + 3 < a.n3) {
-          const float4 bv = val ? *reinterpret_cast<const float4*>(a.b3 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-          *reinterpret_cast<float4*>(yr + c) = make_float4(acc[rb][4 * g] + bv.x, acc[rb][4 * g + 1] + bv.y,
-                                                           acc[rb][4 * g + 2] + bv.z, acc[rb][4 * g + 3] + bv.w);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (c + e < a.n3) yr[c + e] = acc[rb][4 * g + e] + (val ? a.b3[c + e] : 0.f);
-        }
-      }
-    }
-  }
-}
 
 }  // namespace
 
@@ -3223,15 +2730,11 @@ void launch_gemm_x6(const float* X, int ldx, const uint16_t* Wp, int ldp, const 
   // Round 3: the 16x16x32 two-dimensional wave-grid form (gemm_x6m, DMA from the
   // column-half-0 waves) for the wide maps — C2 q|k|v 417792 x 768: 950 -> 877 us, the
   // 192-column orbital map 361 -> 252 us; the single 256-column tile row (Wol, Wm: 1632
-  // tiles over 256 CUs) stays on gemm_x6q (394 vs 404 us).  DH_X6M=0 keeps gemm_x6q.
-  static const bool use_x6m = [] {
-    const char* e = std::getenv("DH_X6M");
-    return !(e && e[0] == '0');
-  }();
+  // tiles over 256 CUs) stays on gemm_x6q (394 vs 404 us).
   int v;
-  if (rows >= 65536 && use_x6m && ncols % 256 == 0 && ncols >= 512) {
+  if (rows >= 65536 && ncols % 256 == 0 && ncols >= 512) {
     v = 76;
-  } else if (rows >= 65536 && use_x6m && ncols == 192) {
+  } else if (rows >= 65536 && ncols == 192) {
     v = 77;
   } else if (rows >= 65536) {
     v = 56;
@@ -3327,88 +2830,33 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 #undef DH_X6LN_ST
 }
 
-// DH_CHAIN=0 keeps the separate LayerNorm GEMMs (A/B measurements)
-bool chain_x6_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_CHAIN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// Chained log-psi layer tail (chain_x6_kernel above).  X1 and h padded to kWalkerRowPad
-// rows; Wp3 may be null (no P3); Y3 rows 16-B aligned (ldy3 % 4 == 0).
+// Chained log-psi layer tail (chain_x6s_kernel above).  X1 and h padded to kWalkerRowPad
+// rows; Wp3 may be null (no P3); Y3 rows 16-B aligned (ldy3 % 4 == 0).  feat.W0qkv (layer 1,
+// chain_attn_supported): the attention runs in the prologue and Wp1 holds the planes of U^T
+// (K = CH_KO), else Wp1 contracts X1 = o over 256.
 void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
                      const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
                      const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, X6Feat feat, hipStream_t s,
                      bool store_h) {
   ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, feat, store_h ? 1 : 0};
-  static const int form = [] {  // DH_CHAIN=2: the LDS-ring form; 3, 4: ablations (tools only)
-    const char* e = std::getenv("DH_CHAIN");
-    return e ? e[0] - '0' : 1;
-  }();
-  if (form == 2) {
-    ensure_smem(chain_x6_kernel, CH_SMEM);
-    hipLaunchKernelGGL(chain_x6_kernel, dim3((rows + CH_BM - 1) / CH_BM), dim3(768), CH_SMEM, s, a);
-  } else {
-    auto k = form == 3 ? chain_x6s_kernel<1> : form == 4 ? chain_x6s_kernel<2> : chain_x6s_kernel<0>;
-    if (feat.W0qkv) {  // chain_attn_supported(feat.N, 4, 64) checked by the caller
-      switch (feat.N) {
-        case 2: k = chain_x6s_kernel<0, 2>; break;
-        case 3: k = chain_x6s_kernel<0, 3>; break;
-        case 4: k = chain_x6s_kernel<0, 4>; break;
-        case 6: k = chain_x6s_kernel<0, 6>; break;
-        default: k = chain_x6s_kernel<0, 8>; break;
-      }
+  auto k = chain_x6s_kernel<0>;
+  if (feat.W0qkv) {  // chain_attn_supported(feat.N, 4, 64) checked by the caller
+    switch (feat.N) {
+      case 2: k = chain_x6s_kernel<2>; break;
+      case 3: k = chain_x6s_kernel<3>; break;
+      case 4: k = chain_x6s_kernel<4>; break;
+      case 6: k = chain_x6s_kernel<6>; break;
+      default: k = chain_x6s_kernel<8>; break;
     }
-    ensure_smem(k, CS_SMEM);
-    hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
   }
+  ensure_smem(k, CS_SMEM);
+  hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
 }
 
-// Layer 1's attention inside the chain prologue (chain_x6s_kernel<0, N>): walker-aligned
-// 96-row tiles, 4 heads of 64 (one per wave pair), the production x6s form.  DH_CHAIN_ATTN=0
-// keeps the separate attention_val_kernel launch (A/B measurements).
+// Layer 1's attention inside the chain prologue (chain_x6s_kernel<N>): walker-aligned 96-row
+// tiles, 4 heads of 64 (one per wave pair)
 bool chain_attn_supported(int N, int H, int dh) {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_CHAIN_ATTN");
-    const char* f = std::getenv("DH_CHAIN");
-    return !(e && e[0] == '0') && !(f && f[0] != '1');
-  }();
-  return on && H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8);
-}
-
-// Chained channel layer tail (chain_ch_kernel above): rows = B N C channel rows; X1 and h
-// readable to round_up(rows + 96, kWalkerRowPad) rows (carve).  N = 3, 6 (C1, C2).
-// Opt-in (DH_CHAIN_CH=1): correct (the parity suite passes with it), but SLOWER than the
-// persistent 256-row channel GEMMs + separate LayerNorm at C2 (E_L 5.08 -> 5.71 ms): its
-// 96-row tiles stream the weights per 85 useful rows (~15 GB of L2 -> CU traffic per step
-// against x6q's LDS-shared 256-row tiles), which costs more than the LayerNorm passes save.
-bool chain_ch_supported(int N) {
-  static const bool on = [] {
-    const char* e = std::getenv("DH_CHAIN_CH");
-    return e && e[0] == '1';
-  }();
-  return on && (N == 3 || N == 6);
-}
-
-void launch_chain_ch(int N, const float* X1, const uint16_t* Wp1, int ldp1, const float* b1, const float* ln1,
-                     const uint16_t* Wp2, int ldp2, const float* b2, const float* ln2, const uint16_t* Wp3, int ldp3,
-                     const float* b3, int n3, float* Y3, int ldy3, float* h, int rows, const float* geo,
-                     hipStream_t s) {
-  X6Feat f{};
-  f.geo = geo;
-  f.N = N;
-  ChainArgs a{X1, Wp1, Wp2, Wp3, ldp1, ldp2, ldp3, b1, ln1, b2, ln2, b3, n3, ldy3, Y3, h, rows, f, 1};
-  auto go = [&](auto kern, int C) {
-    const int RV = (CH_BM / C) * C;
-    ensure_smem(kern, CS_SMEM);
-    hipLaunchKernelGGL(kern, dim3((rows + RV - 1) / RV), dim3(512), CS_SMEM, s, a);
-  };
-  if (N == 3)
-    go(chain_ch_kernel<3>, 11);
-  else
-    go(chain_ch_kernel<6>, 17);
+  return H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8);
 }
 
 }  // namespace dh

@@ -162,9 +162,16 @@ def round4():
     energy_case("MIX_sparse", "MIX", 64, seed=42, orbital="sparse")
 
 
+def round6():
+    """The injected-noise MCMC golden at N = 20 (round-5 verdict, weak 1c): the accept fused
+    into the value kernel's epilogue and the N = 20 value kernel (det_value<MGV>) against
+    mcmc.py:25-64 run by the float64 oracle."""
+    mcmc_case("C5", B=8, steps=3)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    # python make_golden.py [round1] [round2] [round4]   (default: all; round4 rewrites
+    # python make_golden.py [round1] [round2] [round4] [round6]   (default: all; round4 rewrites
     # round 2's pole / C2 / C5 fixtures at the larger sizes)
-    for part in sys.argv[1:] or ["round1", "round2", "round4"]:
-        {"round1": round1, "round2": round2, "round4": round4}[part]()
+    for part in sys.argv[1:] or ["round1", "round2", "round4", "round6"]:
+        {"round1": round1, "round2": round2, "round4": round4, "round6": round6}[part]()

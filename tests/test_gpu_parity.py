@@ -148,11 +148,15 @@ def test_engineered_known_answer_full_batch(cuda, name):
         assert np.median(err) < 2e-6 and np.percentile(err, 99) < 5e-3, k
 
 
-def test_batch_composition_and_chunking_invariance(cuda):
-    ocfg = oracle_config("C2")
+@pytest.mark.parametrize("name,B", [("C2", 37), ("C5", 128)])
+def test_batch_composition_and_chunking_invariance(cuda, name, B):
+    """Rows are independent of the batch and of the workspace chunking, bit for bit.  C5
+    (round-5 verdict, weak 1b): 128 walkers in one chunk against chunks of <= 4 walkers, the
+    N = 20 path (env_stream_kernel at two workgroups per CU, det_value<MGV>)."""
+    ocfg = oracle_config(name)
     system, model = build(ocfg)
     params = to_device_params(make_params(ocfg))
-    x = torch.tensor(make_walkers(37, ocfg.nelec, seed=5), device=cuda)
+    x = torch.tensor(make_walkers(B, ocfg.nelec, seed=5), device=cuda)
     lp_all = model.apply(params, x)
     lp_part = torch.cat([model.apply(params, x[:5]), model.apply(params, x[5:])])
     assert torch.equal(lp_all, lp_part)  # rows are independent: bit-identical
@@ -162,6 +166,7 @@ def test_batch_composition_and_chunking_invariance(cuda):
     h = model.prepare(params, x.device)
     one = h.lib.dh_workspace_bytes(h.h, 4, 1)
     e2, o2 = _run_local_energy(model, params, x, ws_budget=one)  # forces chunks of <= 4 walkers
+    assert torch.isfinite(e1).all()
     assert torch.equal(e1, e2) and torch.equal(o1, o2)
 
 
@@ -179,7 +184,7 @@ def test_nan_and_edge_walkers_propagate(cuda):
     assert torch.equal(e1, e[:1])
 
 
-@pytest.mark.parametrize("name", ["C1", "C2", "C4"])
+@pytest.mark.parametrize("name", ["C1", "C2", "C4", "C5"])
 def test_golden_mcmc_injected_noise(cuda, name):
     g = np.load(GOLDEN / f"mcmc_{name}.npz")
     ocfg = R.OracleConfig(**json.loads(str(g["config"])))
@@ -354,12 +359,14 @@ def test_walker_groups_on_parallel_streams_are_bit_identical(cuda):
                 assert torch.equal(a, b), groups
 
 
-@pytest.mark.parametrize("name,B", [("C2", 4096), ("C4", 1024)])
+@pytest.mark.parametrize("name,B", [("C2", 4096), ("C4", 1024), ("C5", 4096)])
 def test_vmc_iteration_bitwise_repeatable(cuda, name, B):
     """One VMC iteration (4 MCMC moves + the local energy) at the bench's full-chip batch, run
     twice from the same walkers and key: walkers, E_L, observables and accept counts equal bit
     for bit.  A race, an early LDS read or an interleaving-dependent corruption (DESIGN 7.1,
-    the two-tiles-per-CU fused tail) shows here while every small-batch comparison passes."""
+    the two-tiles-per-CU fused tail) shows here while every small-batch comparison passes.
+    C5 at the bench's 4096 walkers runs multi-chunk (its F exceeds one default workspace) and
+    env_stream_kernel at two workgroups per CU (round-5 verdict, weak 1b)."""
     from deephall_amd.random import PRNGKey
     from deephall_amd.train import make_vmc_iteration
 
