@@ -132,6 +132,8 @@ struct dh_handle {
   float* mqk = nullptr;    // layer 1's per-head score forms (attn_val.h, launch_lowrank_qk)
   float* ofw = nullptr;    // layer 1's feature-space output map U^T [256 pad][KO] (launch_ofeat_weight)
   uint16_t* ofp = nullptr;  // its split-bf16 planes [3][x6_plane_rows(D)][KO]
+  float* l1w = nullptr;     // layer 1's coefficient-space maps B^T, V^T (launch_l1_basis)
+  uint16_t* l1p = nullptr;  // their planes
   int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
   bool params_set = false;
@@ -370,6 +372,8 @@ void dh_destroy(dh_handle* h) {
   if (h->mqk) (void)hipFree(h->mqk);
   if (h->ofw) (void)hipFree(h->ofw);
   if (h->ofp) (void)hipFree(h->ofp);
+  if (h->l1w) (void)hipFree(h->l1w);
+  if (h->l1p) (void)hipFree(h->l1p);
   if (h->ref) (void)hipFree(h->ref);
   if (h->wb) (void)hipFree(h->wb);
   if (h->wbt) (void)hipFree(h->wbt);
@@ -447,6 +451,19 @@ int derive_weights(dh_handle* h, hipStream_t st) {
     launch_split_planes(h->ofw, KO, d.D, KO, h->ofp, st);
     h->p.UT = h->ofw;
     h->p.UP = h->ofp;
+    // layer 1 in coefficient space (gemm_lnch MODE 2): B^T, V^T [256 pad][32] and their planes
+    if (d.H == 4) {
+      const size_t nb = (size_t)round_up(d.D, kRowPad) * 32, pb = (size_t)3 * x6_plane_rows(d.D) * 32;
+      if (!h->l1w) HIP_TRY(hipMalloc(&h->l1w, 2 * nb * sizeof(float)));
+      if (!h->l1p) HIP_TRY(hipMalloc(&h->l1p, 2 * pb * sizeof(uint16_t)));
+      HIP_TRY(hipMemsetAsync(h->l1w, 0, 2 * nb * sizeof(float), st));
+      const LayerParams& l0 = h->p.layer[0];
+      launch_l1_basis(d, h->p.W0, h->ofw, l0.bol, l0.ln1, l0.Wm, l0.bm, h->l1w, h->l1w + nb, st);
+      launch_split_planes(h->l1w, 32, d.D, 32, h->l1p, st);
+      launch_split_planes(h->l1w + nb, 32, d.D, 32, h->l1p + pb, st);
+      h->p.L1BP = h->l1p;
+      h->p.L1VP = h->l1p + pb;
+    }
   }
   if (d.D % 32 == 0) {
     // Transposed copies Wt[n][k] (rows zero-padded to 256) of every GEMM weight, for the
@@ -753,6 +770,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
         else
           launch_gemm_ln(w.h, D, lp.WmT, D, lp.bm, lp.ln2, w.h, rows, D, 1, 0, s);
       }
+      continue;
+    }
+    if (lnch && l == 0 && fused && d.H == 4) {
+      // layer 1 whole in one launch from the o~ rows (gemm_lnch MODE 2: LN1, Wm and tanh_ch in
+      // coefficient space, the residual h1 from the same 32-deep rows, LN2)
+      PROF(PK_GEMM + PK_CH, 2.0 * R * DD * 3.0 * KO, f4 * (R * KO + R * DD));
+      launch_gemm_lnch(d.N, w.o, P.UP, x6_plane_rows(D), lp.bol, lp.ln2, w.geo, w.h, nw * d.N, 2, s, P.W0, d.n_up, KO,
+                       P.L1VP, P.L1BP);
       continue;
     }
     if (lnch) {

@@ -1467,6 +1467,35 @@ __global__ void ofeat_weight_kernel(const float* __restrict__ W0qkv, const float
   UT[(size_t)n * KO + k] = (float)s;
 }
 
+// layer 1's coefficient-space maps (gemm_lnch.hip MODE 2): thread (n, j), j < 32
+__global__ void l1_basis_kernel(const float* __restrict__ W0, const float* __restrict__ UT, int KO,
+                                const float* __restrict__ bol, const float* __restrict__ ln1,
+                                const float* __restrict__ Wm, const float* __restrict__ bm, int D,
+                                float* __restrict__ BT, float* __restrict__ VT) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= D * 32) return;
+  const int n = t >> 5, j = t & 31;
+  auto basis = [&](int k) -> double {  // B[j][k]
+    double e;
+    if (j < 4)
+      e = W0[j * D + k];
+    else if (j < 24)
+      e = UT[(size_t)k * KO + 8 * ((j - 4) / 5) + (j - 4) % 5];
+    else if (j == 24)
+      e = bol[k];
+    else if (j == 25)
+      e = 1.0;
+    else
+      return j == 26 ? (double)ln1[D + k] : 0.0;
+    return (double)ln1[k] * e;
+  };
+  double v = j == 26 ? (double)bm[n] : 0.0;
+  if (j <= 26)
+    for (int k = 0; k < D; ++k) v += basis(k) * (double)Wm[(size_t)k * D + n];
+  BT[(size_t)n * 32 + j] = (float)basis(n);
+  VT[(size_t)n * 32 + j] = (float)v;
+}
+
 template <int N>
 void launch_wave(const Dims& d, const float* qkv, const float* W0qkv, const float* bqkv, const float* Mqk,
                  const float* geo, float* o, int nw, int C, hipStream_t s) {
@@ -1518,6 +1547,12 @@ void launch_ofeat_weight(const Dims& d, const float* W0qkv, const float* bqkv, c
   const int n = d.D * 8 * d.H;
   hipLaunchKernelGGL(ofeat_weight_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W0qkv, bqkv, Wol, d.D, d.H,
                      ofeat_k(d), UT);
+}
+
+void launch_l1_basis(const Dims& d, const float* W0, const float* UT, const float* bol, const float* ln1,
+                     const float* Wm, const float* bm, float* BT, float* VT, hipStream_t s) {
+  hipLaunchKernelGGL(l1_basis_kernel, dim3((d.D * 32 + 255) / 256), dim3(256), 0, s, W0, UT, ofeat_k(d), bol, ln1, Wm,
+                     bm, d.D, BT, VT);
 }
 
 void launch_attention(const Dims& d, const float* qkv, const float* geo, float* o, int nw, int C, hipStream_t s,

@@ -51,6 +51,8 @@ struct Params {
   // U[8 h + a][n] = sum_d Wv~[a][h dh + d] Wol[h dh + d][n] (a < 5; a = 5..7 zero), and its planes
   const float* UT;
   const uint16_t* UP;
+  // layer 1 in coefficient space (gemm_lnch MODE 2, H = 4): planes of V^T and B^T [3][ldp][32]
+  const uint16_t *L1VP, *L1BP;
 };
 // Layer 1's attention output in feature space (attention.hip feat2, the chain prologue): per
 // row o~ [ofeat_k] = per head h the five sums o~_h[a] = sum_j A_ij f~_j[a] (f~ = (z, x, y,
@@ -131,11 +133,19 @@ void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, con
 // DH_LNCH=0 selects the GEMM + layernorm_ch pair instead.
 bool gemm_lnch_supported(int N, int D);
 int set_lnch_form(int f);  // 0 off, 1 gemm_lnch_kernel; returns the previous form
-// K: X's row length and the contraction (mode 0 only; 256, or layer 1's ofeat_k o~ rows with
-// Wp = the planes of U^T); mode 1 contracts over h's 256 features.
+// K: X's row length and the contraction (mode 0 / 2; 256, or layer 1's ofeat_k o~ rows with
+// Wp = the planes of U^T); mode 1 contracts over h's 256 features.  Mode 2 (layer 1 whole, H = 4:
+// LN1, Wm, tanh_ch, LN2 from the o~ rows; ln = LN2's scale | shift, bias = bol, W0f = W0): Wv /
+// Wb = the planes of layer 1's coefficient-space maps V^T / B^T (launch_l1_basis, K = 32).
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                       const float* geo, float* h, int ne, int mode, hipStream_t s,
-                      const float* W0f = nullptr, int n_up = 0, int K = 256);
+                      const float* W0f = nullptr, int n_up = 0, int K = 256, const uint16_t* Wv = nullptr,
+                      const uint16_t* Wb = nullptr);
+// Layer 1 in coefficient space (gemm_lnch.hip MODE 2): with E = [W0 (4); U's 5 H nonzero rows;
+// bol; ones] and row 26 = beta, BT[n][j] = gamma_n E[j][n] (j < 26), beta_n (j = 26), and
+// VT[n][j] = sum_k B[j][k] Wm[k][n] (+ bm_n for j = 26); 32 columns, f64 sums; H = 4.
+void launch_l1_basis(const Dims& d, const float* W0, const float* UT, const float* bol, const float* ln1,
+                     const float* Wm, const float* bm, float* BT, float* VT, hipStream_t s);
 bool chain_attn_supported(int N, int H, int dh);
 // Log-psi layer tail in one launch (D = K = 256): h1 = LN1(h + X1 Wol + b1) (feature
 // residual when feat.W0), h = LN2(h1 + tanh(h1 Wm + b2)), then Y3 = h W3 + b3 if Wp3.

@@ -1,7 +1,9 @@
-// Channel-row linear map + channel LayerNorm in ONE launch (local energy, D = K = 256):
+// Channel-row linear map + channel LayerNorm in ONE launch (local energy, D = 256):
 //
 //   MODE 0:  h = LN_ch(h + X W + b)            psiformer.py:44-46  (X = o, W = Wo Wl folded)
 //   MODE 1:  h = LN_ch(h + tanh_ch(h W + b))   psiformer.py:47-48  (X = h)
+//   MODE 2:  layer 1 whole (round 6), from the o~ rows of attention_feat2_kernel:
+//            h = LN_ch2(h1 + tanh_ch(h1 Wm + bm)),  h1 = LN_ch1(f W0 + o~ U + b)
 //
 // in place over h [rows = ne * C][256], C = 2N + 5 channel rows per (walker, electron),
 // bias b on the value rows only; LN_ch / tanh_ch are layernorm.hip's channel rules.  It
@@ -29,53 +31,27 @@
 // 16x16x32 lane groups, checked exhaustively).  Six MFMAs per product block, smallest
 // terms first (as gemm_x6m).
 //
+// MODE 2: layer 1 in coefficient space.  Every pre-LN1 channel row is a combination of 26 fixed
+// vectors: x_c = f_c W0 + o~_c U + [c = 0] b (f_c: the input features' channel seeds, 4; o~_c:
+// the attention's feature-space outputs, 5 per head, dh_internal.h ofeat_k), and centring
+// subtracts mean_c times the all-ones vector, so z_c = zh_c E with E = [W0; U; b; 1] and
+// zh_c = (f_c, o~_c, [c = 0], -mean_c).  LN_ch1's outputs are linear in the z rows with
+// per-electron scalars (s, a_t, cl, au_k, cs_k, computed from the real x rows as MODE 0 does),
+// so h1_c = r_c B with r_c = the same combination of the zh rows and B = [E diag(gamma); beta]
+// (27 rows), and h1_c Wm + bm = r_c V with V = B Wm (+ bm on the beta row): the 256-deep Wm
+// product becomes a 32-deep one over the tile's r rows, and h1 never exists outside the
+// registers.  Passes: o~ U (K = 32) -> LN1 statistics -> r rows into the planes -> r V (K = 32)
+// -> tanh_ch -> += r B (K = 32: the residual h1) -> LN2 -> h.  The weights B, V (planes of B^T,
+// V^T) are formed once per parameter upload (api.cpp, launch_l1_basis, f64 sums).
+//
 // Traffic per launch: X once (the k loop), h once (the epilogue; in MODE 1 the same rows
 // as X, from MALL), h written once: 12 * rows * 256 B, against 20 (MODE 0) / 24 (MODE 1)
-// for the two-kernel form.
-//
-// Build knobs (tools/lnch_one.py A/B builds; defaults are the production kernel):
-// LNCH_COUTER channel-outer k loop; LNCH_SB per-channel sched barrier; LNCH_PF residual
-// loads in flight; LNCH_OPQ opaque residual offsets (register pressure); LNCH_ABL ablations
-// (bit 0: no LayerNorm epilogue, bit 1: no MFMAs — wrong results, timing only); LNCH_RPF MODE 0
-// residual-line touch during the k loop.
+// for the two-kernel form; MODE 2: the o~ rows (128 B per row) read, h written once.
 #include <cstdlib>
 
 #include "dh_internal.h"
 #include "device_common.h"
 
-#ifndef LNCH_COUTER
-#define LNCH_COUTER 0
-#endif
-#ifndef LNCH_SB
-#define LNCH_SB 1
-#endif
-#ifndef LNCH_PF
-#define LNCH_PF 8
-#endif
-#ifndef LNCH_ABL
-#define LNCH_ABL 0
-#endif
-#ifndef LNCH_OPQ
-#define LNCH_OPQ 1
-#endif
-#ifndef LNCH_LBAR  // A/B knob: barriers that wait for LDS only (lgkmcnt(0) + s_barrier), round 5: __syncthreads'
-#define LNCH_LBAR 1  // vmcnt(0) drained the next k-step's activation loads every step and the next residual chunk
-#endif
-#ifndef LNCH_RPF
-#define LNCH_RPF 0
-#endif
-#ifndef LNCH_RDMA
-#define LNCH_RDMA 1
-#endif
-#ifndef LNCH_RDMA_LATE
-#define LNCH_RDMA_LATE 1
-#endif
-#ifndef LNCH_PERMLANE  // round-3 variant kept for the electron-slot study: the
-#define LNCH_PERMLANE 0  // four lane rows' partials summed by permlane32/16 swaps, not in LDS
-#endif
-#ifndef LNCH_LNP  // A/B knob: the LayerNorm scale / shift loaded before the output stores (1) or between them (0)
-#define LNCH_LNP 1
-#endif
 #ifndef LNCH_STAMP
 #define LNCH_STAMP 0
 #endif
@@ -108,39 +84,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
+constexpr int LN_NWV = 8;   // waves per workgroup (one workgroup per CU)
 constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
-constexpr int LN_D = 256;   // features (= K)
+constexpr int LN_D = 256;   // features (= K of MODE 1)
 constexpr int LN_BK = 32;   // k per step
-// epilogue residual through LDS (LNCH_RDMA): chunks of LN_RCH channel rows of all 16
-// electrons (LN_RCH * 16 rows of 1 KB).  LNCH_R3 (round 5): 3-row chunks in three buffers —
-// two over the stage area, the third past the geometry, free during the k loop, so chunk 0 is
-// requested at kernel start (its latency hides behind the first k-step's own loads) and two
-// chunks are in flight behind the one being added; else 4-row chunks in two buffers
-#ifndef LNCH_R3
-#define LNCH_R3 0  // measured neutral (profiles/r05_v13_ab.txt): kept off
-#endif
-constexpr int LN_RCH = LNCH_R3 ? 3 : 4;
-constexpr int LN_NBUF = LNCH_R3 ? 3 : 2;
+constexpr int LN_KB = 32;   // MODE 2: coefficient-row length (27 used: 4 + 5 H + 3, H = 4)
+// epilogue residual through LDS: chunks of LN_RCH channel rows of all 16 electrons (LN_RCH * 16
+// rows of 1 KB) in two buffers over the stage area
+constexpr int LN_RCH = 4;
 constexpr int LN_RBUF = LN_RCH * LN_EPT * LN_D * 4;  // bytes of one chunk buffer
 
-// LDS bytes of the kernel: the two k-step plane stages (reused by the epilogue's residual
-// chunks and statistics), then the walkers' geometry, then (LNCH_R3) the third chunk buffer
+__host__ __device__ constexpr int lnch_nr(int N) { return (2 * N + 5) + 2 * N + 3; }  // second moments
+__host__ __device__ constexpr int lnch_ts(int N) { return lnch_nr(N) | 1; }          // odd stride
+// LDS bytes: the two k-step plane stages / the residual chunk buffers (the epilogue's reduction
+// scratch and totals, then MODE 2's zh rows), then the walkers' geometry
 __host__ __device__ constexpr int lnch_geo_off(int N) {
-  return (6 * (2 * N + 5) * LN_EPT * 64 > (LNCH_RDMA ? 2 * LN_RBUF : 0)) ? 6 * (2 * N + 5) * LN_EPT * 64
-                                                                       : 2 * LN_RBUF;
+  return (6 * (2 * N + 5) * LN_EPT * 64 > 2 * LN_RBUF) ? 6 * (2 * N + 5) * LN_EPT * 64 : 2 * LN_RBUF;
 }
-__host__ __device__ constexpr int lnch_bx_off(int N) {
-  return (lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16 + 1023) & ~1023;
-}
-__host__ __device__ constexpr int lnch_smem(int N) {
-  return (LNCH_RDMA && LN_NBUF == 3) ? lnch_bx_off(N) + LN_RBUF
-                                     : lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16;
-}
-// byte offset of chunk k's buffer
-__host__ __device__ constexpr int lnch_cbuf(int N, int k) {
-  return LN_NBUF == 3 ? (k % 3 == 0 ? lnch_bx_off(N) : (k % 3 - 1) * LN_RBUF) : (k & 1) * LN_RBUF;
+__host__ __device__ constexpr int lnch_smem(int N) { return lnch_geo_off(N) + ((LN_EPT + N - 1) / N + 1) * N * 16; }
+__host__ __device__ constexpr int lnch_z_off(int N) {
+  return (LN_NWV * lnch_nr(N) * 64 * 4 + LN_EPT * lnch_ts(N) * 4 + 15) & ~15;
 }
 
 __device__ __forceinline__ uint32_t pkbf(float x, float y) {
@@ -149,37 +113,88 @@ __device__ __forceinline__ uint32_t pkbf(float x, float y) {
 __device__ __forceinline__ float lo_of(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_of(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ int lnch_sw(int e) { return (0x78 >> (2 * ((e >> 2) & 3))) & 3; }
-#if LNCH_PERMLANE
-// sum over the four lanes e, e + 16, e + 32, e + 48 (the round-3 permlane form)
-__device__ __forceinline__ float lnch_sum4g(float v) {
-  const int x = __float_as_int(v);
-  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  v = __int_as_float(a[0]) + __int_as_float(a[1]);
-  const int y = __float_as_int(v);
-  const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);
-  return __int_as_float(b[0]) + __int_as_float(b[1]);
+// 4 consecutive k values of one (channel, electron) row as their three bf16 terms, at byte
+// offset loff of each plane (the k-step plane image above)
+__device__ __forceinline__ void put_split4(char* P, int plane, int loff, float x, float y, float z, float w) {
+  const uint32_t h0 = pkbf(x, y), h1 = pkbf(z, w);
+  const float rx = x - lo_of(h0), ry = y - hi_of(h0), rz = z - lo_of(h1), rw = w - hi_of(h1);
+  const uint32_t m0 = pkbf(rx, ry), m1 = pkbf(rz, rw);
+  const uint32_t s0 = pkbf(rx - lo_of(m0), ry - hi_of(m0)), s1 = pkbf(rz - lo_of(m1), rw - hi_of(m1));
+  *reinterpret_cast<uint2*>(P + loff) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(P + plane + loff) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(P + 2 * plane + loff) = make_uint2(s0, s1);
 }
-#endif
+// input.hip's channel seed f_c of electron ie (geometry st ct sp cp) for channel c
+template <int N>
+__device__ __forceinline__ float4 chan_feature(int c, int ie, float4 g4, int n_up) {
+  constexpr int T = 2 * N;
+  const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+  const float rx = st * cp, ry = st * sp, rz = ct;
+  float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c == 0) {
+    f = make_float4(rz, rx, ry, (ie < n_up) ? 1.f : -1.f);
+  } else if (c <= T) {
+    const int t = c - 1;
+    if ((t >> 1) == ie) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
+  } else if (c == T + 1) {
+    f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
+  } else {
+    const int k = c - T - 2;  // 0:x 1:y 2:z
+    f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
+  }
+  return f;
+}
+// flow coefficient alpha_kt (layernorm.hip) from the walker's geometry gw[electron]
+__device__ __forceinline__ float alpha_of(const float4* gw, int k, int t) {
+  const float4 q = gw[t >> 1];
+  if ((t & 1) == 0) return k == 0 ? -q.z : (k == 1 ? q.w : 0.f);
+  return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
+}
+// the channel LayerNorm's per-electron scalars from its second moments mt (lnch_nr of them:
+// <z0 z_c>, <z_t^2>, <u_k^2>)
+template <int N>
+struct LnScalars {
+  float s, s2, cl, aL, au[3], cs[3];
+  __device__ __forceinline__ void from(const float* mt, const float4* gw) {
+    constexpr int C = 2 * N + 5, T = 2 * N;
+    s = 1.f / sqrtf(mt[0] + 1e-5f);
+    s2 = s * s;
+    cl = 0.f;
+    au[0] = au[1] = au[2] = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float a = s2 * mt[1 + t];
+      cl += 3.f * a * a - s2 * mt[C + t];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) au[k] = fmaf(alpha_of(gw, k, t), a, au[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cs[k] = 3.f * au[k] * au[k] - s2 * mt[C + T + k];
+    aL = s2 * mt[1 + T];
+  }
+};
 
-template <int N, int MODE, int NWV, bool FRES = false>
-__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >= 8 ? 2 : 1, NWV >= 8 ? 2 : 1))) void gemm_lnch_kernel(const float* X, const uint16_t* __restrict__ Wp, int ldp,
-                                                         const float* __restrict__ bias,
-                                                         const float* __restrict__ ln,
-                                                         const float* __restrict__ geo, float* h, int ne,
-                                                         const float* __restrict__ W0f, int n_up, int kx) {
-  // K: the contraction length = X's row length, a multiple of BK (256; MODE 0 of layer 1 from
-  // the o~ rows: ofeat_k, dh_internal.h); a compile-time 256 in MODE 1
-  constexpr int C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, BK = LN_BK;
+template <int N, int MODE, bool FRES = false>
+__global__ __launch_bounds__(LN_NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_lnch_kernel(
+    const float* X, const uint16_t* __restrict__ Wp, int ldp, const float* __restrict__ bias,
+    const float* __restrict__ ln, const float* __restrict__ geo, float* h, int ne, const float* __restrict__ W0f,
+    int n_up, int kx, const uint16_t* __restrict__ Wv, const uint16_t* __restrict__ Wb) {
+  // K: the contraction length = X's row length, a multiple of BK (256; layer 1 from the o~
+  // rows: ofeat_k, dh_internal.h); a compile-time 256 in MODE 1
+  constexpr int NWV = LN_NWV, C = 2 * N + 5, T = 2 * N, EPT = LN_EPT, D = LN_D, BK = LN_BK;
   const int K = MODE == 1 ? LN_D : kx, NK = K / BK;
   constexpr int ROWS = EPT * C;                    // activation rows per tile
   constexpr int NT = NWV * 64, CB = D / (16 * NWV);  // threads; 16-column blocks per wave
   constexpr int PLANE = C * EPT * 64;              // bytes of one bf16 plane per step
   constexpr int STAGE = 3 * PLANE;
   constexpr int NQ = (ROWS * 8 + NT - 1) / NT;     // 16-B activation pieces per thread per step
-  constexpr int NR = C + T + 3;                    // second-moment statistics per electron
-  constexpr int TS = NR | 1;                       // odd row stride of the totals
+  constexpr int NR = lnch_nr(N);                   // second-moment statistics per electron
+  constexpr int TS = lnch_ts(N);
+  constexpr int KB = LN_KB;
   static_assert(2 * STAGE <= lnch_geo_off(N) && lnch_smem(N) <= 163840, "LDS");
   static_assert(NWV * NR * 64 * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
+  static_assert(MODE != 2 || lnch_z_off(N) + EPT * C * KB * 4 <= lnch_geo_off(N), "MODE 2 zh rows");
+  static_assert(MODE != 2 || NWV * NR * 64 * 4 >= STAGE, "MODE 2: the r planes stay clear of the totals");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -189,13 +204,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   // every barrier here orders LDS only (planes, residual chunks after their counted DMA waits,
   // statistics): global loads in flight may cross it
   auto lbar = []() __attribute__((always_inline)) {
-#if LNCH_LBAR
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-#else
-    __syncthreads();
-#endif
   };
   const int e0 = tile * EPT;                       // first electron of the tile
   const size_t row0 = (size_t)e0 * C;
@@ -214,7 +225,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   // ---- activation pieces of this thread: piece i = tid + NT j -> (row i >> 3, quad i & 7)
   // buffer descriptor over the tile's activation rows (tile-uniform base; rows past the last
   // electron are out of range: their loads return 0)
-  const uint32_t tbytes = (uint32_t)rows_valid * D * 4, xbytes = (uint32_t)rows_valid * K * 4;
+  const uint32_t xbytes = (uint32_t)rows_valid * K * 4;
   const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X) + row0 * K, (short)0, xbytes, 0x00020000);
   int goff[NQ], loff[NQ];
 #pragma unroll
@@ -237,13 +248,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     for (int j = 0; j < NQ; ++j) {
       if (loff[j] < 0) continue;
       const float4 u = ra[j];
-      const uint32_t h0 = pkbf(u.x, u.y), h1 = pkbf(u.z, u.w);
-      const float rx = u.x - lo_of(h0), ry = u.y - hi_of(h0), rz = u.z - lo_of(h1), rw = u.w - hi_of(h1);
-      const uint32_t m0 = pkbf(rx, ry), m1 = pkbf(rz, rw);
-      const uint32_t s0 = pkbf(rx - lo_of(m0), ry - hi_of(m0)), s1 = pkbf(rz - lo_of(m1), rw - hi_of(m1));
-      *reinterpret_cast<uint2*>(P + loff[j]) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(P + PLANE + loff[j]) = make_uint2(m0, m1);
-      *reinterpret_cast<uint2*>(P + 2 * PLANE + loff[j]) = make_uint2(s0, s1);
+      put_split4(P, PLANE, loff[j], u.x, u.y, u.z, u.w);
     }
   };
   // ---- weight fragments of this wave: feature n = 16 (CB wid + cb) + l16, k = 32 kt + 8 kg
@@ -256,16 +261,14 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   };
   const int xoff = l16 * 64 + ((kg ^ lnch_sw(l16)) * 16);  // + c * EPT * 64 within a plane
 
-#if LNCH_RDMA
   // ---- the residual rows h through LDS by DMA (global_load_lds_dwordx4, no VGPRs): chunk k =
   // channel rows LN_RCH k .. + LN_RCH - 1 of the tile's 16 electrons, one 1-KB row per wave
-  // instruction, into chunk buffer lnch_cbuf(k) at row q = (c - LN_RCH k) * 16 + e.  16-B slot s of
+  // instruction, into chunk buffer k & 1 at row q = (c - LN_RCH k) * 16 + e.  16-B slot s of
   // a row holds the row's quad s ^ e (the swizzle is on the SOURCE address: the DMA writes
   // lane-linearly), so the epilogue's ds_read_b128 of quad Q = 8 w + 4 cb + g by lane (e, g)
   // hits slot Q ^ e: 16 distinct slots in every lane group.  Rows of electrons past the end
   // re-read the tile's first row into their (never read) slot, so every wave issues the same
-  // compile-time number of DMAs per chunk and "chunk k landed" is vmcnt(DMAs of the younger
-  // chunks k + 1 .. k + LN_NBUF - 1).
+  // compile-time number of DMAs per chunk and "chunk k landed" is vmcnt(DMAs of chunk k + 1).
   constexpr int NCHK = (C + LN_RCH - 1) / LN_RCH;
   auto rows_of = [](int k) { return EPT * (C - LN_RCH * k < LN_RCH ? C - LN_RCH * k : LN_RCH); };
   static_assert(EPT * LN_RCH % NWV == 0 && EPT % NWV == 0, "DMA rows must divide over the waves");
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         const int le = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         uint32_t voff = (uint32_t)(le ^ e) << 4;
         asm volatile("" : "+v"(voff));
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(lnch_cbuf(N, k) + q * D * 4));
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((k & 1) * LN_RBUF + q * D * 4));
         unsigned keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
@@ -293,11 +296,9 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       }
     }
   };
-  // MODE 0 of layer 1 (W0f): the residual h0 = f W0 is formed from the walkers' geometry in the
-  // epilogue (round 5), so h0 is never written by the input kernel nor read back here
-  constexpr bool fres = MODE == 0 && FRES;
-  if (LN_NBUF == 3 && !fres) rdma(0);  // LNCH_R3: chunk 0 into the buffer past the stages, now
-#endif
+  // layer 1 (MODE 0 with W0f, MODE 2): the residual h0 = f W0 is formed from the walkers'
+  // geometry in the epilogue (round 5), so h0 is never written by the input kernel nor read back
+  constexpr bool fres = (MODE == 0 && FRES) || MODE == 2;
   // the accumulators start from zero (the residual is added in the epilogue: starting them
   // from h rounds every k-step's partial sum at |h| and measurably loosened the tangent
   // channels against float64 on ill-conditioned walkers)
@@ -307,73 +308,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
   {
-#if LNCH_COUTER
-    // channel outermost: each activation fragment read from LDS once per step and used by
-    // all CB column blocks (half the LDS reads of the block-outer order); all CB blocks'
-    // weight fragments live, the next step's streaming in behind them
-    float4 ra[NQ];
-    bf16x8 wf[CB][3], wn[CB][3];
-    load_a(0, ra);
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) load_w(0, cb, wf[cb]);
-    split_store(ra, 0);
-    if (NK > 1) load_a(1, ra);
-#pragma unroll 1
-    for (int kt = 0; kt < NK; ++kt) {
-      lbar();  // planes of step kt complete; step kt - 1's buffer is free
-      const char* P = smem + (kt & 1) * STAGE + xoff;
-      if (kt + 1 < NK) {
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb) load_w(kt + 1, cb, wn[cb]);
-      }
-      bf16x8 xf[2][3];
-      auto ldx = [&](int c, bf16x8 (&x)[3]) {
-        x[0] = *reinterpret_cast<const bf16x8*>(P + c * EPT * 64);
-        x[1] = *reinterpret_cast<const bf16x8*>(P + PLANE + c * EPT * 64);
-        x[2] = *reinterpret_cast<const bf16x8*>(P + 2 * PLANE + c * EPT * 64);
-      };
-      ldx(0, xf[0]);
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        if (c + 1 < C) ldx(c + 1, xf[(c + 1) & 1]);  // one channel ahead
-        const bf16x8 x0 = xf[c & 1][0], x1 = xf[c & 1][1], x2 = xf[c & 1][2];
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          f32x4 a = acc[c][cb];
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x2, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][2], x0, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][1], x1, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x1, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][1], x0, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][0], x0, a, 0, 0, 0);
-          acc[c][cb] = a;
-        }
-        if (c == C / 2 && kt + 1 < NK) {
-          split_store(ra, (kt + 1) & 1);
-          if (kt + 2 < NK) load_a(kt + 2, ra);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (kt + 1 < NK) {
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) wf[cb][p] = wn[cb][p];
-      }
-    }
-  }
-#else
     // column block outermost: one block's weight fragments (12 VGPRs) live at a time, the next
     // block's streaming in behind them; the activation fragments are re-read from LDS per block
     float4 ra[NQ];
     bf16x8 wf[3], wn[3];
-    // MODE 0 (X = o, not h): one dword of every 128-B line of the tile's residual rows is
-    // touched during the k loop (one line per thread per step), so the epilogue's residual
-    // loads find the lines in the MALL / L2 instead of HBM; the touched values are folded
-    // into an opaque word, consumed a step later (the load never stalls the loop)
-    constexpr int RLINES = ROWS * D * 4 / 128;
-    const auto rsH = __builtin_amdgcn_make_buffer_rsrc(h + row0 * D, (short)0, tbytes, 0x00020000);
-    uint32_t rpf = 0, rpv = 0;
     load_a(0, ra);
     load_w(0, 0, wf);
     split_store(ra, 0);
@@ -404,9 +342,6 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           if (c + 1 < C) ldx(c + 1, xf[(c + 1) & 1]);  // one channel ahead
           const bf16x8 x0 = xf[c & 1][0], x1 = xf[c & 1][1], x2 = xf[c & 1][2];
           f32x4 a = acc[c][cb];
-#if LNCH_ABL & 2
-          if (a[0] == 1.2345e-33f)  // ablation (tools only): MFMAs skipped
-#endif
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x2, a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], x0, a, 0, 0, 0);
           a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x1, a, 0, 0, 0);
@@ -417,36 +352,23 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
           if (cb == 0 && c == C / 2 && kt + 1 < NK) {
             split_store(ra, (kt + 1) & 1);
             if (kt + 2 < NK) load_a(kt + 2, ra);
-            if (MODE == 0 && LNCH_RPF) {
-              rpf ^= rpv;
-              const int li = kt * NT + tid;
-              rpv = li < RLINES ? __builtin_amdgcn_raw_buffer_load_b32(rsH, li * 128, 0, 0) : 0u;
-            }
           }
-#if LNCH_SB
           __builtin_amdgcn_sched_barrier(0);
-#endif
         }
 #pragma unroll
         for (int p = 0; p < 3; ++p) wf[p] = wn[p];
       }
     }
-    if (MODE == 0 && LNCH_RPF && (rpf ^ rpv) == 0x7fc00001u && ne < 0) h[0] = 0.f;  // never taken
   }
-#endif
   lbar();  // every wave is past its last plane read: the stage buffers become scratch
   LNCH_T(2);
   // the epilogue's lane indices, re-derived from the lane id (mbcnt) rather than kept live
   // across the k loop from threadIdx (holding them there made MODE 1 spill)
   const int lane_e = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#if LNCH_RDMA
-  if ((MODE == 0 || !LNCH_RDMA_LATE) && !fres) {
-    if (LN_NBUF == 2) rdma(0);
-#pragma unroll
-    for (int x = 1; x < LN_NBUF; ++x)
-      if (x < NCHK) rdma(x);
+  if (MODE == 0 && !fres) {
+    rdma(0);
+    if (NCHK > 1) rdma(1);
   }
-#endif
   const int l16e = lane_e & 15, kge = lane_e >> 4, tide = wid * 64 + lane_e;
   // lane = electron l16 of the tile; its accumulators hold features nf + 16 cb + 0..3 of every
   // channel row (MFMA D layout: col = lane & 15, row = 4 (lane >> 4) + reg)
@@ -464,43 +386,20 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     asm volatile("" : "+v"(o));
     return o;
   };
-#if !LNCH_RDMA
-  auto ldh = [&](int c, int cb) { return *reinterpret_cast<const float4*>(htile + roff(c, cb)); };
-#endif
   auto sth = [&](int c, int cb, float4 v) {
     if (valid) *reinterpret_cast<float4*>(htile + roff(c, cb)) = v;
   };
-#if LNCH_ABL & 1
-  {  // ablation (tools only): no LayerNorm epilogue, the raw accumulators stored
-    const int E = e0 + l16;
-    if (E < ne) {
-      float* hr = h + (row0 + (size_t)l16 * C) * D + 16 * CB * wid + 4 * kg;
-      for (int c = 0; c < C; ++c)
-        for (int cb = 0; cb < CB; ++cb) *reinterpret_cast<f32x4*>(hr + c * D + 16 * cb) = acc[c][cb];
-    }
-    return;
-  }
-#endif
 
   // ---- epilogue: lane = electron l16, features nf + 16 cb + 0..3 of every channel row
   // geometry of the walker's electrons (st, ct, sp, cp) from the tile's LDS copy (read where
   // used: holding N float4 per lane would spill the accumulators)
   const float4* gw = gl + (b - e0 / N) * N;
-  auto al = [&](int k, int t) -> float {  // flow coefficient alpha_kt (layernorm.hip)
-    const float4 q = gw[t >> 1];
-    if ((t & 1) == 0) return k == 0 ? -q.z : (k == 1 ? q.w : 0.f);
-    return k == 0 ? -(q.y * q.w) : (k == 1 ? -(q.y * q.z) : q.x);
-  };
-  // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
+  // tanh_ch of the pre-activation rows in acc (layernorm.hip: y0 = tanh z0, y_t = d1 z_t,
+  // y_L = d1 z_L + d2 sum_t z_t^2, y_Sk = d1 z_Sk + d2 u_k^2)
   float chain = 0.f;
+  auto tanh_ch = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int cb = 0; cb < CB; ++cb) {
-    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-    acc[0][cb][0] += bv.x;
-    acc[0][cb][1] += bv.y;
-    acc[0][cb][2] += bv.z;
-    acc[0][cb][3] += bv.w;
-    if (MODE == 1) {
+    for (int cb = 0; cb < CB; ++cb) {
       // the value row's tanh first, one feature at a time (its temporaries never overlap
       // the channel algebra's); tanh_ocml = tanhf bit for bit, without tanhf's branch
 #pragma unroll
@@ -535,30 +434,33 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+  };
+  // pre-LN rows x_c (in acc): bias (value rows), MODE 1's tanh_ch, then + h
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[0][cb][0] += bv.x;
+    acc[0][cb][1] += bv.y;
+    acc[0][cb][2] += bv.z;
+    acc[0][cb][3] += bv.w;
   }
-#if LNCH_RDMA
-  if (MODE == 1) {
+  if constexpr (MODE == 1) {
+    tanh_ch();
     // the tanh_ch results are materialised here, before the DMA blocks (otherwise the
     // compiler sinks the channel algebra past them and its live ranges spill)
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) asm volatile("" : "+v"(acc[c][cb]));
-  }
-  if (MODE == 1 && LNCH_RDMA_LATE) {
-    if (LN_NBUF == 2) rdma(0);
-#pragma unroll
-    for (int x = 1; x < LN_NBUF; ++x)
-      if (x < NCHK) rdma(x);
+    rdma(0);
+    if (NCHK > 1) rdma(1);
   }
   if constexpr (fres) {
     // input.hip's channel features of this lane's electron (the geometry staged in gl) times
     // W0's columns nf + 16 cb .. + 3, the input kernel's expression, then added as the
     // residual rows are (r + acc)
     const float4 g4 = gl[valid ? E - (e0 / N) * N : 0];  // st ct sp cp
-    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
     const int ie = (valid ? E : e0) % N;
-    const float rx = st * cp, ry = st * sp, rz = ct;
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
       const float4 w0 = *reinterpret_cast<const float4*>(W0f + nf + 16 * cb);
@@ -567,18 +469,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
       const float4 w3 = *reinterpret_cast<const float4*>(W0f + 3 * D + nf + 16 * cb);
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c == 0) {
-          f = make_float4(rz, rx, ry, (ie < n_up) ? 1.f : -1.f);
-        } else if (c <= T) {
-          const int t = c - 1;
-          if ((t >> 1) == ie) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
-        } else if (c == T + 1) {
-          f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
-        } else {
-          const int k = c - T - 2;  // 0:x 1:y 2:z
-          f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
-        }
+        const float4 f = chan_feature<N>(c, ie, g4, n_up);
         f32x4& a = acc[c][cb];
         a[0] = (f.x * w0.x + f.y * w1.x + f.z * w2.x + f.w * w3.x) + a[0];
         a[1] = (f.x * w0.y + f.y * w1.y + f.z * w2.y + f.w * w3.y) + a[1];
@@ -594,13 +485,10 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     for (int cb = 0; cb < CB; ++cb) rsl[cb] = 16 * ((4 * CB * wid + 4 * cb + kge) ^ l16e);
 #pragma unroll
     for (int k = 0; k < NCHK; ++k) {
-      // this wave's chunk-k DMAs landed (the younger ones are chunks k + 1 .. k + LN_NBUF - 1,
-      // issued before this wait), then every wave's
-      const int YNG = (k + 1 < NCHK ? rows_of(k + 1) : 0) / NWV + (LN_NBUF == 3 && k + 2 < NCHK ? rows_of(k + 2) : 0) / NWV;
-      if (YNG > 0)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((k + 1 < NCHK ? rows_of(k + 1) : 0) / NWV +
-                                                (LN_NBUF == 3 && k + 2 < NCHK ? rows_of(k + 2) : 0) / NWV)
-                     : "memory");
+      // this wave's chunk-k DMAs landed (the younger ones are chunk k + 1's, issued before this
+      // wait), then every wave's
+      if (k + 1 < NCHK)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((k + 1 < NCHK ? rows_of(k + 1) : 0) / NWV) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lbar();
@@ -610,50 +498,24 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
         if (c < C) {
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) {
-            const float4 r = *reinterpret_cast<const float4*>(rb0 + lnch_cbuf(N, k) + cc * EPT * D * 4 + rsl[cb]);
+            const float4 r = *reinterpret_cast<const float4*>(rb0 + (k & 1) * LN_RBUF + cc * EPT * D * 4 + rsl[cb]);
             f32x4& a = acc[c][cb];
             a[0] = r.x + a[0];
             a[1] = r.y + a[1];
             a[2] = r.z + a[2];
             a[3] = r.w + a[3];
-#if LNCH_OPQ
             asm volatile("" : "+v"(a));  // consumed here (keeps the reads from being batched)
-#endif
           }
         }
       }
-      if (k + LN_NBUF < NCHK) {
+      if (k + 2 < NCHK) {
         lbar();  // every wave is done with chunk k's buffer
-        rdma(k + LN_NBUF);
+        rdma(k + 2);
       }
     }
     lbar();  // the chunk buffers become the statistics scratch
     LNCH_T(3);
   }
-#else
-  static_assert(!fres, "the feature residual needs the LNCH_RDMA build (the default)");
-  {
-    // residual rows, PF float4 loads in flight (ldh's opaque offsets keep the compiler from
-    // hoisting all C * CB of them, which would spill the accumulators)
-    constexpr int NRES = C * CB, PF = LNCH_PF;
-    float4 rb[PF];
-#pragma unroll
-    for (int i = 0; i < PF && i < NRES; ++i) rb[i] = ldh(i / CB, i % CB);
-#pragma unroll
-    for (int i = 0; i < NRES; ++i) {
-      const float4 r = rb[i % PF];
-      if (i + PF < NRES) rb[i % PF] = ldh((i + PF) / CB, (i + PF) % CB);
-      f32x4& a = acc[i / CB][i % CB];
-      a[0] = r.x + a[0];
-      a[1] = r.y + a[1];
-      a[2] = r.z + a[2];
-      a[3] = r.w + a[3];
-#if LNCH_OPQ
-      asm volatile("" : "+v"(a));  // consumed here, before the next load is issued
-#endif
-    }
-  }
-#endif
   float* red = reinterpret_cast<float*>(smem);   // [NWV waves][NR][64 lanes] partial sums
   float* tot = red + NWV * NR * 64;               // [EPT][TS] totals (odd stride: 16 banks)
   auto lane_sum = [&](int c) {
@@ -667,12 +529,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     constexpr int NS = decltype(NS_)::value;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-#if LNCH_PERMLANE
-      const float v = lnch_sum4g(part(j));
-      if (kge == 0) red[(wid * NS + j) * 64 + l16e] = v;
-#else
       red[(wid * NS + j) * 64 + lane_e] = part(j);  // every lane's 8-feature partial (no cross-lane ops)
-#endif
       __builtin_amdgcn_sched_barrier(0);          // one statistic at a time (register pressure)
     }
     lbar();
@@ -682,31 +539,30 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
 #pragma unroll
       for (int w = 0; w < NWV; ++w)
 #pragma unroll
-        for (int g = 0; g < (LNCH_PERMLANE ? 1 : 4); ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
+        for (int g = 0; g < 4; ++g) s += red[(w * NS + j) * 64 + 16 * g + e];
       tot[e * TS + j] = s * (1.f / D);
     }
     lbar();
   };
   const float* mt = tot + l16e * TS;  // this lane's electron
-  // channel means, centre
-  reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
-  LNCH_T(4);
+  auto center = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float mu = mt[c];
+    for (int c = 0; c < C; ++c) {
+      const float mu = mt[c];
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
+      for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) acc[c][cb][v] -= mu;
-    __builtin_amdgcn_sched_barrier(0);
-  }
+        for (int v = 0; v < 4; ++v) acc[c][cb][v] -= mu;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   // flow vector u_k = sum_t alpha_kt z_t of columns block cb (recomputed where needed)
   auto flow = [&](int k, int cb) {
     f32x4 r = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       if (k == 2 && (t & 1) == 0) continue;  // alpha_2,2i = 0
-      const float a = al(k, t);
+      const float a = alpha_of(gw, k, t);
       r[0] = fmaf(a, acc[1 + t][cb][0], r[0]);
       r[1] = fmaf(a, acc[1 + t][cb][1], r[1]);
       r[2] = fmaf(a, acc[1 + t][cb][2], r[2]);
@@ -716,49 +572,161 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   };
   auto dot4 = [](const f32x4& x, const f32x4& y) { return (x[0] * y[0] + x[1] * y[1]) + (x[2] * y[2] + x[3] * y[3]); };
   // p_c = <z0 z_c>, q_t = <z_t^2>, uu_k = <u_k^2>
-  reduce(
-      [&](int j) {
-        float r = 0.f;
+  auto reduce2 = [&]() __attribute__((always_inline)) {
+    reduce(
+        [&](int j) {
+          float r = 0.f;
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          if (j < C) {
-            r += dot4(acc[0][cb], acc[j][cb]);
-          } else if (j < C + T) {
-            r += dot4(acc[1 + j - C][cb], acc[1 + j - C][cb]);
-          } else {
-            const f32x4 u = flow(j - C - T, cb);
-            r += dot4(u, u);
+          for (int cb = 0; cb < CB; ++cb) {
+            if (j < C) {
+              r += dot4(acc[0][cb], acc[j][cb]);
+            } else if (j < C + T) {
+              r += dot4(acc[1 + j - C][cb], acc[1 + j - C][cb]);
+            } else {
+              const f32x4 u = flow(j - C - T, cb);
+              r += dot4(u, u);
+            }
           }
-        }
-        return r;
-      },
-      std::integral_constant<int, NR>{});
-  LNCH_T(5);
-  const float s = 1.f / sqrtf(mt[0] + 1e-5f), s2 = s * s;
-  float cl = 0.f, au[3] = {0.f, 0.f, 0.f};
+          return r;
+        },
+        std::integral_constant<int, NR>{});
+  };
+  // channel means, centre
+  reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
+  LNCH_T(4);
+  if constexpr (MODE == 2) {
+    // ---- zh rows (header): thread (e, c) -> Z[e][c][0..31] = (f_c, o~_c (5 per head), [c = 0],
+    // -mean_c, 0 ...), o~ re-read from global memory (the tile's rows, L2-resident)
+    float* Z = reinterpret_cast<float*>(smem + lnch_z_off(N));
+    if (tid < EPT * C) {
+      const int e = tid / C, c = tid - (tid / C) * C;
+      const int Ee = e0 + e;
+      const float4 g4 = gl[Ee < ne ? Ee - (e0 / N) * N : 0];
+      const float4 f = chan_feature<N>(c, (Ee < ne ? Ee : e0) % N, g4, n_up);
+      float* zr = Z + (e * C + c) * KB;
+      *reinterpret_cast<float4*>(zr) = f;
+      const int ro = (e * C + c) * K * 4;  // bytes from the tile's first o~ row (range-checked)
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const float a = s2 * mt[1 + t];
-    cl += 3.f * a * a - s2 * mt[C + t];
+      for (int hh = 0; hh < 4; ++hh) {
+        const float4 o4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsX, ro + 32 * hh, 0, 0));
+        const float o5 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, ro + 32 * hh + 16, 0, 0));
+        zr[4 + 5 * hh] = o4.x;
+        zr[5 + 5 * hh] = o4.y;
+        zr[6 + 5 * hh] = o4.z;
+        zr[7 + 5 * hh] = o4.w;
+        zr[8 + 5 * hh] = o5;
+      }
+      zr[24] = c == 0 ? 1.f : 0.f;
+      zr[25] = -tot[e * TS + c];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) au[k] = fmaf(al(k, t), a, au[k]);
+      for (int j = 26; j < KB; ++j) zr[j] = 0.f;
+    }
+    // (the next barrier is reduce2's, after every lane's partials are written)
   }
-  float cs[3];
+  center();
+  reduce2();
+  LNCH_T(5);
+  if constexpr (MODE == 2) {
+    // ---- r rows: thread (e, c) forms LN_ch1's combination of the zh rows (the output block's
+    // formulas below, with z -> zh) and writes it into plane buffer 0 as the next B operand
+    {
+      const float* Z = reinterpret_cast<const float*>(smem + lnch_z_off(N));
+      if (tid < EPT * C) {
+        const int e = tid / C, c = tid - (tid / C) * C;
+        const int Ee = e0 + e;
+        const float4* gwe = gl + ((Ee < ne ? Ee : e0) / N - e0 / N) * N;
+        LnScalars<N> S;
+        S.from(tot + e * TS, gwe);
+        const float* me = tot + e * TS;
+        const float* z0 = Z + (e * C) * KB;
+        const float* zc = Z + (e * C + c) * KB;
+        char* P = smem;  // plane buffer 0 (clear of the totals: static_assert above)
+#pragma unroll 1
+        for (int q = 0; q < KB / 4; ++q) {
+          float r[4];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) cs[k] = 3.f * au[k] * au[k] - s2 * mt[C + T + k];
-  const float aL = s2 * mt[1 + T];
+          for (int v = 0; v < 4; ++v) {
+            const int j = 4 * q + v;
+            float y;
+            if (c == 0) {
+              y = S.s * z0[j];
+            } else if (c <= T) {
+              y = S.s * (zc[j] - (S.s2 * me[c]) * z0[j]);
+            } else if (c == T + 1) {
+              float sat = 0.f;
+              for (int t = 0; t < T; ++t) sat = fmaf(S.s2 * me[1 + t], Z[(e * C + 1 + t) * KB + j], sat);
+              y = S.s * (zc[j] - S.aL * z0[j] - 2.f * sat + S.cl * z0[j]);
+            } else {
+              const int k = c - T - 2;
+              float uk = 0.f;
+              for (int t = 0; t < T; ++t) uk = fmaf(alpha_of(gwe, k, t), Z[(e * C + 1 + t) * KB + j], uk);
+              const float ak = S.s2 * me[2 + T + k];
+              y = S.s * (zc[j] - ak * z0[j] - 2.f * S.au[k] * uk + S.cs[k] * z0[j]);
+            }
+            if (j == 26) y = c == 0 ? 1.f : 0.f;  // the beta row
+            r[v] = y;
+          }
+          put_split4(P, PLANE, (c * EPT + e) * 64 + (((q >> 1) ^ lnch_sw(e)) * 16) + (q & 1) * 8, r[0], r[1], r[2], r[3]);
+        }
+      }
+    }
+    lbar();
+    // ---- 32-deep passes over the r planes (buffer 0): acc (+)= r W^T, W = Wv or Wb planes
+    const int xo = l16e * 64 + ((kge ^ lnch_sw(l16e)) * 16);
+    auto pass = [&](const uint16_t* __restrict__ Wq) __attribute__((always_inline)) {
+      const uint16_t* wq = Wq + (size_t)(16 * CB * wid + l16e) * KB + 8 * kge;
+      const size_t wpl = (size_t)ldp * KB;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        asm volatile("" ::: "memory");
+        bf16x8 wf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wf[p] = *reinterpret_cast<const bf16x8*>(wq + p * wpl + (size_t)cb * 16 * KB);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const char* P = smem + xo + c * EPT * 64;
+          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(P);
+          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(P + PLANE);
+          const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(P + 2 * PLANE);
+          f32x4 a = acc[c][cb];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x2, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x1, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], x0, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], x0, a, 0, 0, 0);
+          acc[c][cb] = a;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    pass(Wv);   // the pre-activation h1 Wm + bm (bm on the beta row of V)
+    tanh_ch();
+    pass(Wb);   // + h1 (beta on the beta row of B)
+    lbar();     // every wave is past its plane reads: the reduction scratch overlaps them
+    reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
+    center();
+    reduce2();
+  }
+  LnScalars<N> S;
+  S.from(mt, gw);
+  const float s = S.s;
   // the LayerNorm scale / shift of both column blocks before the first store: a load between
   // two stores waits for every earlier store (vmcnt counts in order)
   float4 lng[CB], lnb[CB];
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
-    lng[cb] = LNCH_LNP ? *reinterpret_cast<const float4*>(ln + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-    lnb[cb] = LNCH_LNP ? *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    lng[cb] = *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
+    lnb[cb] = *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb);
   }
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
-    const float4 gv = LNCH_LNP ? lng[cb] : *reinterpret_cast<const float4*>(ln + nf + 16 * cb);
-    const float4 bb = LNCH_LNP ? lnb[cb] : *reinterpret_cast<const float4*>(ln + D + nf + 16 * cb);
+    const float4 gv = lng[cb];
+    const float4 bb = lnb[cb];
     const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bq[4] = {bb.x, bb.y, bb.z, bb.w};
     float gs[4], z0[4];
 #pragma unroll
@@ -771,7 +739,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     float sat[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float at = s2 * mt[1 + t];
+      const float at = S.s2 * mt[1 + t];
       float y[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -785,17 +753,17 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
     {
       float y[4];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) y[v] = gs[v] * (acc[1 + T][cb][v] - aL * z0[v] - 2.f * sat[v] + cl * z0[v]);
+      for (int v = 0; v < 4; ++v) y[v] = gs[v] * (acc[1 + T][cb][v] - S.aL * z0[v] - 2.f * sat[v] + S.cl * z0[v]);
       sth(1 + T, cb, make_float4(y[0], y[1], y[2], y[3]));
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const f32x4 uk = flow(k, cb);
-      const float ak = s2 * mt[2 + T + k];
+      const float ak = S.s2 * mt[2 + T + k];
       float y[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v)
-        y[v] = gs[v] * (acc[2 + T + k][cb][v] - ak * z0[v] - 2.f * au[k] * uk[v] + cs[k] * z0[v]);
+        y[v] = gs[v] * (acc[2 + T + k][cb][v] - ak * z0[v] - 2.f * S.au[k] * uk[v] + S.cs[k] * z0[v]);
       sth(2 + T + k, cb, make_float4(y[0], y[1], y[2], y[3]));
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -804,30 +772,25 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV >=
   LNCH_RT(9);
 }
 
-template <int N, int NWV>
-void launch_lnch_t(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
-  const size_t smem = lnch_smem(N);
-  const int grid = (ne + LN_EPT - 1) / LN_EPT;
-  if (mode == 0 && W0f) {
-    ensure_smem(gemm_lnch_kernel<N, 0, NWV, true>, smem);
-    hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV, true>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo,
-                       h, ne, W0f, n_up, K);
-  } else if (mode == 0) {
-    ensure_smem(gemm_lnch_kernel<N, 0, NWV>, smem);
-    hipLaunchKernelGGL((gemm_lnch_kernel<N, 0, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne, W0f, n_up, K);
-  } else {
-    ensure_smem(gemm_lnch_kernel<N, 1, NWV>, smem);
-    hipLaunchKernelGGL((gemm_lnch_kernel<N, 1, NWV>), dim3(grid), dim3(NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h,
-                       ne, nullptr, 0, LN_D);
-  }
-}
-
 template <int N>
 void launch_lnch_n(const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln, const float* geo,
-                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
-  launch_lnch_t<N, 8>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K);
+                   float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K, const uint16_t* Wv,
+                   const uint16_t* Wb) {
+  const size_t smem = lnch_smem(N);
+  const int grid = (ne + LN_EPT - 1) / LN_EPT;
+  auto go = [&](auto kern) {
+    ensure_smem(kern, smem);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(LN_NWV * 64), smem, s, X, Wp, ldp, bias, ln, geo, h, ne, W0f, n_up, K, Wv,
+                       Wb);
+  };
+  if (mode == 2)
+    go(gemm_lnch_kernel<N, 2>);
+  else if (mode == 0 && W0f)
+    go(gemm_lnch_kernel<N, 0, true>);
+  else if (mode == 0)
+    go(gemm_lnch_kernel<N, 0>);
+  else
+    go(gemm_lnch_kernel<N, 1>);
 }
 
 }  // namespace
@@ -855,18 +818,19 @@ bool gemm_lnch_supported(int N, int D) {
 }
 
 void launch_gemm_lnch(int N, const float* X, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
-                      const float* geo, float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K) {
-  if (mode != 0) {
+                      const float* geo, float* h, int ne, int mode, hipStream_t s, const float* W0f, int n_up, int K,
+                      const uint16_t* Wv, const uint16_t* Wb) {
+  if (mode == 1) {
     W0f = nullptr;
     K = LN_D;
   }
   switch (N) {
-    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
-    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
-    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
-    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
-    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
-    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K); return;
+    case 1: launch_lnch_n<1>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
+    case 2: launch_lnch_n<2>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
+    case 3: launch_lnch_n<3>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
+    case 4: launch_lnch_n<4>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
+    case 5: launch_lnch_n<5>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
+    default: launch_lnch_n<6>(X, Wp, ldp, bias, ln, geo, h, ne, mode, s, W0f, n_up, K, Wv, Wb); return;
   }
 }
 
