@@ -55,22 +55,26 @@
 #ifndef LNCH_STAMP
 #define LNCH_STAMP 0
 #endif
+#ifndef LNCH_STAMP_MODE  // stamp builds: only launches of this MODE write (-1: every launch)
+#define LNCH_STAMP_MODE -1
+#endif
 
 namespace dh {
 
 #if LNCH_STAMP
 // diagnostic builds only (tools/lnch_one.py): per-workgroup phase timestamps (s_memtime) of
 // the first LNCH_STAMP_WG tiles, written by thread 0 into a buffer nothing else reads
-constexpr int LNCH_STAMP_WG = 4096, LNCH_NSTAMP = 10;
+// (slots 0-6 the phases, 8-9 real time at start / end; MODE 2 also 10-14)
+constexpr int LNCH_STAMP_WG = 4096, LNCH_NSTAMP = 16;
 __device__ unsigned long long g_lnch_stamp[LNCH_STAMP_WG * LNCH_NSTAMP];
 #define LNCH_T(i)                                                                    \
   do {                                                                               \
-    if (threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG)                              \
+    if ((LNCH_STAMP_MODE < 0 || LNCH_STAMP_MODE == MODE) && threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG) \
       g_lnch_stamp[blockIdx.x * LNCH_NSTAMP + (i)] = __builtin_amdgcn_s_memtime();   \
   } while (0)
 #define LNCH_RT(i)                                                                   \
   do {                                                                               \
-    if (threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG)                              \
+    if ((LNCH_STAMP_MODE < 0 || LNCH_STAMP_MODE == MODE) && threadIdx.x == 0 && blockIdx.x < LNCH_STAMP_WG) \
       g_lnch_stamp[blockIdx.x * LNCH_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
@@ -90,6 +94,7 @@ constexpr int LN_EPT = 16;  // electrons per tile (the MFMA column dimension)
 constexpr int LN_D = 256;   // features (= K of MODE 1)
 constexpr int LN_BK = 32;   // k per step
 constexpr int LN_KB = 32;   // MODE 2: coefficient-row length (27 used: 4 + 5 H + 3, H = 4)
+constexpr int LN_SCF = 32;  // MODE 2: floats of one electron's LN_ch1 scalar table (8 + T <= 32)
 // epilogue residual through LDS: chunks of LN_RCH channel rows of all 16 electrons (LN_RCH * 16
 // rows of 1 KB) in two buffers over the stage area
 constexpr int LN_RCH = 4;
@@ -193,7 +198,8 @@ __global__ __launch_bounds__(LN_NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 
   constexpr int KB = LN_KB;
   static_assert(2 * STAGE <= lnch_geo_off(N) && lnch_smem(N) <= 163840, "LDS");
   static_assert(NWV * NR * 64 * 4 + EPT * TS * 4 <= 2 * STAGE, "reduction scratch");
-  static_assert(MODE != 2 || lnch_z_off(N) + EPT * C * KB * 4 <= lnch_geo_off(N), "MODE 2 zh rows");
+  static_assert(MODE != 2 || lnch_z_off(N) + (EPT * C * KB + EPT * LN_SCF) * 4 <= lnch_geo_off(N), "MODE 2 zh rows");
+  static_assert(MODE != 2 || (EPT * KB == NT && 8 + T <= LN_SCF), "MODE 2: thread (electron, column)");
   static_assert(MODE != 2 || NWV * NR * 64 * 4 >= STAGE, "MODE 2: the r planes stay clear of the totals");
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
@@ -627,50 +633,64 @@ __global__ __launch_bounds__(LN_NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 
   reduce2();
   LNCH_T(5);
   if constexpr (MODE == 2) {
-    // ---- r rows: thread (e, c) forms LN_ch1's combination of the zh rows (the output block's
-    // formulas below, with z -> zh) and writes it into plane buffer 0 as the next B operand
+    // ---- r rows: LN_ch1's combinations of the zh rows (the output block's formulas below, with
+    // z -> zh), written into plane buffer 0 as the next B operand.  First the per-electron
+    // scalars into a table past the zh rows (thread e), then thread (e, j) forms column j of
+    // every channel row of electron e: C + 4 T FMAs from C zh values, no serial chains.
     {
       const float* Z = reinterpret_cast<const float*>(smem + lnch_z_off(N));
-      if (tid < EPT * C) {
-        const int e = tid / C, c = tid - (tid / C) * C;
-        const int Ee = e0 + e;
+      float* SC = reinterpret_cast<float*>(smem + lnch_z_off(N)) + EPT * C * KB;  // [EPT][LN_SCF]
+      if (tid < EPT) {
+        const int Ee = e0 + tid;
         const float4* gwe = gl + ((Ee < ne ? Ee : e0) / N - e0 / N) * N;
-        LnScalars<N> S;
-        S.from(tot + e * TS, gwe);
-        const float* me = tot + e * TS;
-        const float* z0 = Z + (e * C) * KB;
-        const float* zc = Z + (e * C + c) * KB;
-        char* P = smem;  // plane buffer 0 (clear of the totals: static_assert above)
-#pragma unroll 1
-        for (int q = 0; q < KB / 4; ++q) {
-          float r[4];
+        LnScalars<N> S1;
+        S1.from(tot + tid * TS, gwe);
+        float* sc = SC + tid * LN_SCF;
+        sc[0] = S1.s;
+        sc[1] = S1.aL - S1.cl;  // y_L = s (z_L - (aL - cl) z0 - 2 sum_t a_t z_t)
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int j = 4 * q + v;
-            float y;
-            if (c == 0) {
-              y = S.s * z0[j];
-            } else if (c <= T) {
-              y = S.s * (zc[j] - (S.s2 * me[c]) * z0[j]);
-            } else if (c == T + 1) {
-              float sat = 0.f;
-              for (int t = 0; t < T; ++t) sat = fmaf(S.s2 * me[1 + t], Z[(e * C + 1 + t) * KB + j], sat);
-              y = S.s * (zc[j] - S.aL * z0[j] - 2.f * sat + S.cl * z0[j]);
-            } else {
-              const int k = c - T - 2;
-              float uk = 0.f;
-              for (int t = 0; t < T; ++t) uk = fmaf(alpha_of(gwe, k, t), Z[(e * C + 1 + t) * KB + j], uk);
-              const float ak = S.s2 * me[2 + T + k];
-              y = S.s * (zc[j] - ak * z0[j] - 2.f * S.au[k] * uk + S.cs[k] * z0[j]);
-            }
-            if (j == 26) y = c == 0 ? 1.f : 0.f;  // the beta row
-            r[v] = y;
-          }
-          put_split4(P, PLANE, (c * EPT + e) * 64 + (((q >> 1) ^ lnch_sw(e)) * 16) + (q & 1) * 8, r[0], r[1], r[2], r[3]);
+        for (int k = 0; k < 3; ++k) {
+          sc[2 + k] = S1.s2 * tot[tid * TS + 2 + T + k] - S1.cs[k];  // y_Sk = s (z_Sk - (ak - cs_k) z0 - 2 au_k u_k)
+          sc[5 + k] = 2.f * S1.au[k];
         }
+#pragma unroll
+        for (int t = 0; t < T; ++t) sc[8 + t] = S1.s2 * tot[tid * TS + 1 + t];  // a_t
       }
+      lbar();
+      const int e = tid >> 5, j = tid & 31, Ee = e0 + e;
+      const float4* gwe = gl + ((Ee < ne ? Ee : e0) / N - e0 / N) * N;
+      const float* sc = SC + e * LN_SCF;
+      const float* zc = Z + (e * C) * KB + j;  // + c KB
+      const float sv = sc[0], z0 = zc[0];
+      float sat = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+      char* P = smem;  // plane buffer 0 (clear of the totals: static_assert above)
+      const int lo = e * 64 + ((((j >> 2) >> 1) ^ lnch_sw(e)) * 16) + ((j >> 2) & 1) * 8 + (j & 3) * 2;
+      auto put = [&](int c, float y) __attribute__((always_inline)) {  // element (c, e, k = j), three bf16 terms
+        const uint32_t h2 = pkbf(y, 0.f);
+        const float ry = y - lo_of(h2);
+        const uint32_t m2 = pkbf(ry, 0.f);
+        const uint32_t l2 = pkbf(ry - lo_of(m2), 0.f);
+        char* q = P + c * EPT * 64 + lo;
+        *reinterpret_cast<uint16_t*>(q) = (uint16_t)h2;
+        *reinterpret_cast<uint16_t*>(q + PLANE) = (uint16_t)m2;
+        *reinterpret_cast<uint16_t*>(q + 2 * PLANE) = (uint16_t)l2;
+      };
+      put(0, j == 26 ? 1.f : sv * z0);  // row 26: the beta row (zh has 0 there)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float zt = zc[(1 + t) * KB], at = sc[8 + t];
+        sat = fmaf(at, zt, sat);
+        u0 = fmaf(alpha_of(gwe, 0, t), zt, u0);
+        u1 = fmaf(alpha_of(gwe, 1, t), zt, u1);
+        if (t & 1) u2 = fmaf(alpha_of(gwe, 2, t), zt, u2);
+        put(1 + t, sv * (zt - at * z0));
+      }
+      put(1 + T, sv * (zc[(1 + T) * KB] - sc[1] * z0 - 2.f * sat));
+      const float uk[3] = {u0, u1, u2};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) put(2 + T + k, sv * (zc[(2 + T + k) * KB] - sc[2 + k] * z0 - sc[5 + k] * uk[k]));
     }
-    lbar();
+    LNCH_T(10);    lbar();
     // ---- 32-deep passes over the r planes (buffer 0): acc (+)= r W^T, W = Wv or Wb planes
     const int xo = l16e * 64 + ((kge ^ lnch_sw(l16e)) * 16);
     auto pass = [&](const uint16_t* __restrict__ Wq) __attribute__((always_inline)) {
@@ -705,12 +725,16 @@ __global__ __launch_bounds__(LN_NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) acc[c][cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
     pass(Wv);   // the pre-activation h1 Wm + bm (bm on the beta row of V)
+    LNCH_T(11);
     tanh_ch();
+    LNCH_T(12);
     pass(Wb);   // + h1 (beta on the beta row of B)
     lbar();     // every wave is past its plane reads: the reduction scratch overlaps them
+    LNCH_T(13);
     reduce([&](int c) { return lane_sum(c); }, std::integral_constant<int, C>{});
     center();
     reduce2();
+    LNCH_T(14);
   }
   LnScalars<N> S;
   S.from(mt, gw);
