@@ -745,6 +745,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
         feat.W0qkv = P.W0qkv;
         feat.bqkv = lp.bqkv;
         feat.Mqk = P.Mqk;
+        feat.L1V = P.L1VP;
+        feat.L1B = P.L1BP;
       }
       // layer 1 with its attention in the prologue: P1 contracts the o~ planes with U (K = 32)
       launch_chain_x6(w.o, attn_in_chain ? P.UP : lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D),

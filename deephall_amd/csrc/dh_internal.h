@@ -124,6 +124,9 @@ struct X6Feat {
   const float* W0qkv = nullptr;
   const float* bqkv = nullptr;
   const float* Mqk = nullptr;  // [H][kMqkStride] (attn_val.h attn_feat_core)
+  // with W0qkv: layer 1's coefficient-space maps (planes of V^T, B^T; launch_l1_basis)
+  const uint16_t* L1V = nullptr;
+  const uint16_t* L1B = nullptr;
 };
 void launch_gemm_x6_ln(const float* X, int ldx, const uint16_t* Wp, int ldp, const float* bias, const float* ln,
                        float* h, int rows, int K, int mode, int nw, hipStream_t s, X6Feat feat = X6Feat{});

@@ -1994,6 +1994,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   constexpr int RB = CS_RB, PD = CS_PD, LSP = CS_LSP;
   using K16 = std::integral_constant<int, CH_K / 16>;                     // a 256-deep pass
   using KP1 = std::integral_constant<int, (NA > 0 ? CH_KO / 16 : CH_K / 16)>;  // P1: o~ (layer 1) or o
+  using K2 = std::integral_constant<int, 2>;  // layer 1's coefficient-space passes (32 deep)
   extern __shared__ float4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   float* part = reinterpret_cast<float*>(smem + 3 * CS_PLANE);  // [2][8 waves][96 rows]
@@ -2063,7 +2064,8 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       for (int p = 0; p < 3; ++p) bq[d][p] = *reinterpret_cast<const bf16x8*>(wr + p * plane + 16 * d);
   };
   // TR: the operands swapped, D[tile row][output column] (P3's store layout, CHAIN_P3T)
-  auto gemm = [&](auto tr_, auto nkt_) __attribute__((always_inline)) {
+  // accumulate_: keep acc's contents (layer 1's residual pass, NA > 0) instead of starting from 0
+  auto gemm = [&](auto tr_, auto nkt_, auto accumulate_) __attribute__((always_inline)) {
     constexpr bool TR = decltype(tr_)::value;
     constexpr int nk = decltype(nkt_)::value;
     auto mf = [](const bf16x8& w, const bf16x8& x, const f32x16& c) __attribute__((always_inline)) {
@@ -2072,10 +2074,12 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       else
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, x, c, 0, 0, 0);
     };
+    if constexpr (!decltype(accumulate_)::value) {
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+      for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[rb][e] = 0.f;
+        for (int e = 0; e < 16; ++e) acc[rb][e] = 0.f;
+    }
     // A fragments of k-tile kt (rows 32 rb + l32, k = 16 kt + 8 lh ..), read one k-tile ahead
     bf16x8 ca[RB][3];
     auto lda = [&](int kt, bf16x8(&d)[RB][3]) __attribute__((always_inline)) {
@@ -2122,6 +2126,8 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     }
   };
   using NoTr = std::integral_constant<bool, false>;
+  using Zero = std::integral_constant<bool, false>;
+  using Accum = std::integral_constant<bool, true>;
   // MFMA layout: reg 4 g + e of acc[rb] = tile row 32 rb + l32, column 32 wid + 8 g + 4 lh + e
   auto colof = [&](int g) __attribute__((always_inline)) { return 32 * wid + 8 * g + 4 * lh; };
   // LayerNorm of the values x (MFMA layout, 16 per lane and row block) in registers:
@@ -2304,7 +2310,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   }
   // ---- P1: h1 = LN1(h + o Wol + bol) -> planes
   CHAIN_T(1);
-  gemm(NoTr{}, KP1{});
+  gemm(NoTr{}, KP1{}, Zero{});
   CHAIN_T(2);
   {
     // every load of this phase issued before the first use, and P2's weight prefetch after
@@ -2327,7 +2333,10 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
         gq[rb] = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)r);  // st ct sp cp
       }
       __builtin_amdgcn_sched_barrier(0);  // the residual loads ahead of the prefetch in vmcnt's queue
-      prefetch(a.Wp2, a.ldp2, 0, K16{});
+      if constexpr (NA > 0)
+        prefetch(a.feat.L1V, a.ldp2, 0, K2{});
+      else
+        prefetch(a.Wp2, a.ldp2, 0, K16{});
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const int r = row0 + 32 * rb + l32;
@@ -2381,6 +2390,101 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     }
   }
   CHAIN_T(3);
+  if constexpr (NA > 0) {
+    // ---- layer 1 in coefficient space (gemm_lnch.hip MODE 2's header with C = 1): the row
+    // x = f W0 + o~ U + bol is (f, o~, 1) E, so LN1(x) = gamma * rs ((f, o~, 1, -mean) E) + beta
+    // = r B with r = rs (f, o~, 1, -mean) and the beta row, and h1 Wm + bm = r V: P2's 256-deep
+    // pass becomes two 32-deep ones over r (V, then B accumulated onto tanh: the residual h1),
+    // and neither h1 nor its planes are formed.  LN1's statistics as layernorm() (one round).
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      float t = 0.f, q = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        t += (x[rb][4 * g] + x[rb][4 * g + 1]) + (x[rb][4 * g + 2] + x[rb][4 * g + 3]);
+        q += (x[rb][4 * g] * x[rb][4 * g] + x[rb][4 * g + 1] * x[rb][4 * g + 1]) +
+             (x[rb][4 * g + 2] * x[rb][4 * g + 2] + x[rb][4 * g + 3] * x[rb][4 * g + 3]);
+      }
+      t += __shfl_xor(t, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lh == 0) {
+        part[wid * CH_BM + 32 * rb + l32] = t;
+        part[(CS_NW + wid) * CH_BM + 32 * rb + l32] = q;
+      }
+    }
+    lbar();
+    // row table (mean, rs) in plane 0's columns 32.. of each row (past the o~ columns)
+    if (wid == 0 && lh == 0) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        float t = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < CS_NW; ++w) {
+          t += part[w * CH_BM + 32 * rb + l32];
+          q += part[(CS_NW + w) * CH_BM + 32 * rb + l32];
+        }
+        const float mean = t * (1.f / 256.f);
+        const float var = fmaxf(q * (1.f / 256.f) - mean * mean, 0.f);
+        *reinterpret_cast<float2*>(pl(0, 32 * rb + l32, 32)) = make_float2(mean, __builtin_amdgcn_rsqf(var + 1e-5f));
+      }
+    }
+    lbar();
+    // thread (row, j): r[j] for rows tid / 32 + 16 p; every read before any plane write
+    constexpr int RP = CH_BM / 16;
+    const int j = tid & 31;
+    float rv[RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int r = (tid >> 5) + 16 * p, grow = min(row0 + r, rows - 1);
+      const float2 st = *reinterpret_cast<const float2*>(pl(0, r, 32));  // mean, rs
+      float z = 0.f;
+      if (j < 4) {
+        const float4 g = *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)grow);  // st ct sp cp
+        z = j == 0 ? g.y : (j == 1 ? g.x * g.w : (j == 2 ? g.x * g.z : ((grow % a.feat.N < a.feat.n_up) ? 1.f : -1.f)));
+      } else if (j < 24) {
+        const int c = 8 * ((j - 4) / 5) + (j - 4) % 5;  // o~ column of (head, slot)
+        const uint32_t h = *reinterpret_cast<const uint16_t*>(pl(0, r, c));
+        const uint32_t m = *reinterpret_cast<const uint16_t*>(pl(1, r, c));
+        const uint32_t l = *reinterpret_cast<const uint16_t*>(pl(2, r, c));
+        z = (lo_f(h) + lo_f(m)) + lo_f(l);
+      } else if (j == 24) {
+        z = 1.f;
+      } else if (j == 25) {
+        z = -st.x;
+      }
+      rv[p] = j == 26 ? 1.f : st.y * z;  // row 26: the beta row (unscaled)
+    }
+    lbar();
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      const int r = (tid >> 5) + 16 * p;
+      const float v = rv[p];
+      const uint32_t h2 = pk_bf16(v, 0.f);
+      const float rx = v - lo_f(h2);
+      const uint32_t m2 = pk_bf16(rx, 0.f);
+      const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
+      *reinterpret_cast<uint16_t*>(pl(0, r, j)) = (uint16_t)h2;
+      *reinterpret_cast<uint16_t*>(pl(1, r, j)) = (uint16_t)m2;
+      *reinterpret_cast<uint16_t*>(pl(2, r, j)) = (uint16_t)l2;
+    }
+    lbar();
+    CHAIN_T(4);
+    // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) with h1 Wm + bm = r V, h1 = r B
+    CHAIN_T(5);
+    gemm(NoTr{}, K2{}, Zero{});
+    prefetch(a.feat.L1B, a.ldp2, 0, K2{});
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[rb][e] = tanh_rat(acc[rb][e]);
+    gemm(NoTr{}, K2{}, Accum{});
+    CHAIN_T(6);
+    if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0, K16{});
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) x[rb][e] = acc[rb][e];
+  } else {
   layernorm(CHAIN_PRM ? prm : a.ln1);  // its barriers: every wave is past its GEMM reads of the planes
   CHAIN_T(4);
 #pragma unroll
@@ -2391,7 +2495,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   lbar();
   // ---- P2: h2 = LN2(h1 + tanh(h1 Wm + bm)) -> planes and h
   CHAIN_T(5);
-  gemm(NoTr{}, K16{});
+  gemm(NoTr{}, K16{}, Zero{});
   CHAIN_T(6);
   if (a.Wp3 && 32 * wid < a.n3) prefetch(a.Wp3, a.ldp3, 0, K16{});
 #pragma unroll
@@ -2410,6 +2514,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       x[rb][4 * g + 2] = h1.z + th(acc[rb][4 * g + 2] + bv.z);
       x[rb][4 * g + 3] = h1.w + th(acc[rb][4 * g + 3] + bv.w);
     }
+  }
   CHAIN_T(7);
   layernorm(CHAIN_PRM ? prm + 768 : a.ln2);
   CHAIN_T(8);
@@ -2429,7 +2534,7 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
   // ---- P3: Y3 = h2 W3 + b3, 256-column passes (a wave past n3 idles), MFMA-layout stores
   for (int col0 = 0; col0 < a.n3; col0 += CH_BN) {
     if (col0 + 32 * wid >= a.n3) continue;  // wave-uniform
-    gemm(std::integral_constant<bool, CHAIN_P3T != 0>{}, K16{});
+    gemm(std::integral_constant<bool, CHAIN_P3T != 0>{}, K16{}, Zero{});
     if (col0 < 3 * CH_BN) CHAIN_T(10 + 2 * (col0 / CH_BN));
 #if CHAIN_P3T
     {  // D[tile row][column]: reg q of acc[rb] = row 32 rb + (q & 3) + 8 (q >> 2) + 4 lh, column l32.
