@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--extra-configs", default="C4,C5",
                     help="comma list of EXTRA_CONFIGS also timed (one-GPU lines in configs_1gpu; '' = none)")
     ap.add_argument("--extra-steps", type=int, default=3)
+    ap.add_argument("--extra-mcmc-calls", type=int, default=5,
+                    help="timed mcmc_step calls for the C4 / C5 lines' walker_steps_per_sec")
     ap.add_argument("--extra-warmup", type=int, default=2)
     ap.add_argument("--cpu-c1-seconds", type=float, default=6.0,
                     help="CPU-baseline budget for BASELINE.json configs[0] (N=3 2Q=2, B=100)")
@@ -92,7 +94,8 @@ def spawn_ranks(n: int) -> int:
 EXTRA_CONFIGS = {"C4": ((10, 0), 23), "C5": ((20, 0), 57)}  # BASELINE.json configs[3], [4]
 
 
-def run_workload(args, dev, rank, world, nspins, flux, B, n_steps, n_warmup, burn_in, instrument, components):
+def run_workload(args, dev, rank, world, nspins, flux, B, n_steps, n_warmup, burn_in, instrument, components,
+                 mcmc_calls=None):
     """One workload: burn-in, W warmup VMC steps, exactly K timed steps (barrier + sync on both
     sides, max over ranks), then the instrumented region and the component timings."""
     from deephall_amd import _lib, config
@@ -186,10 +189,11 @@ def run_workload(args, dev, rank, world, nspins, flux, B, n_steps, n_warmup, bur
     # ---------------- MCMC walker-steps/s: >= 20 mcmc_step calls, each with
     # its pmove all-reduce and the host read of pmove; then the E_L-only rate
     t_mcmc = t_el = float("nan")
+    mcmc_calls = mcmc_calls or args.mcmc_calls
     if components:
         barrier()
         a = time.perf_counter()
-        for _ in range(args.mcmc_calls):
+        for _ in range(mcmc_calls):
             data, pm = mcmc_step(params, data, key, width)
             float(pm)  # device sync, as pmove.item() in update_mcmc_width
             key = key.advance(steps)
@@ -198,7 +202,7 @@ def run_workload(args, dev, rank, world, nspins, flux, B, n_steps, n_warmup, bur
         tm = torch.tensor([t_mcmc], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        t_mcmc = float(tm.item()) / args.mcmc_calls
+        t_mcmc = float(tm.item()) / mcmc_calls
         a = time.perf_counter()
         for _ in range(3):
             _run_local_energy(model, params, data)
@@ -235,13 +239,15 @@ def roofline_of(prof, n_steps, dt_prof, x6, traffic=None, traffic_src=None):
 
     g_cnt, g_ms, g_fl, g_by = _cls("gemm_ch")
     l_cnt, l_ms, l_fl, l_by = _cls("gemm")
+    f_cnt, f_ms, f_fl, f_by = _cls("layer1_ch")
     achieved = (g_fl / (g_ms * 1e-3)) / 1e12 if g_ms > 0 else 0.0
     peak = PEAK_BF16_MFMA_TFLOPS / 6 if x6 else PEAK_F32_MFMA_TFLOPS
     return {
-        "kernel": ("local-energy channel GEMMs, split-bf16 f32 GEMM (v_mfma_f32_16x16x32_bf16): "
-                   "gemm_x6m_kernel (q|k|v and orbital maps) + gemm_lnch_kernel (the 256-column maps "
-                   "with the channel LayerNorm fused in; its LN work counted in the launch time, not "
-                   "in the flops), averaged over the 6 launches"
+        "kernel": ("local-energy channel GEMMs (the 256-deep ones), split-bf16 f32 GEMM "
+                   "(v_mfma_f32_16x16x32_bf16): gemm_x6m_kernel (layer 2's q|k|v and the orbital map) + "
+                   "gemm_lnch_kernel (layer 2's two 256-column maps with the channel LayerNorm fused in; "
+                   f"its LN work counted in the launch time, not in the flops), averaged over the "
+                   f"{g_cnt / n_steps:g} launches per step"
                    if x6 else "gemm_ntp_kernel (exact-f32 channel GEMMs)"),
         "bound": "mfma",
         "achieved": round(achieved, 2),
@@ -258,6 +264,11 @@ def roofline_of(prof, n_steps, dt_prof, x6, traffic=None, traffic_src=None):
         "measured_over": f"{n_steps} instrumented VMC steps (HIP event pair per launch)",
         "traffic_source": traffic_src,
         "bytes_per_launch_algorithmic": g_by / g_cnt if g_cnt else 0,
+        "layer1_ch": {  # gemm_lnch MODE 2: layer 1 whole (LayerNorms, tanh, three 32-deep products)
+            "launches_per_step": f_cnt / n_steps,
+            "avg_launch_us": 1e3 * f_ms / f_cnt if f_cnt else 0,
+            "share_of_step": round(f_ms / (dt_prof * 1e3), 4) if f_ms else None,
+        } if f_cnt else None,
         "logpsi_gemms": {
             "launches_per_step": l_cnt / n_steps,
             "avg_launch_us": 1e3 * l_ms / l_cnt if l_cnt else 0,
@@ -304,7 +315,7 @@ def main():
         for tag in args.extra_configs.split(","):
             nsp, fx = EXTRA_CONFIGS[tag]
             rx = run_workload(args, dev, rank, world, nsp, fx, B, args.extra_steps, args.extra_warmup, 2,
-                              not args.no_kernel_events, False)
+                              not args.no_kernel_events, not args.no_components, args.extra_mcmc_calls)
             extra[tag] = (nsp, fx, rx)
 
     if rank != 0:
@@ -325,6 +336,24 @@ def main():
         traffic = tj.get("channel_gemm_bytes_per_launch") if x6 else None
         traffic_src = f"profiles/gemm_traffic.json ({tj.get('tag', '?')})" if traffic else None
     roofline = roofline_of(prof, args.steps, dt_prof, x6, traffic, traffic_src) if not args.no_kernel_events else None
+    # MFMA utilisation of the same kernels: rocprofv3 PMC SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8
+    # x 1024 SIMDs) of this workload (tools/pmc_mfma.py, committed by tools/profile_round.sh)
+    mf = ROOT / "profiles" / "mfma_pmc.json"
+    if roofline and mf.exists() and (B, tuple(args.nspins), args.flux, steps) == (4096, (6, 0), 15, 10):
+        mj = json.loads(mf.read_text())
+        ks = mj.get("kernels", {})
+
+        def busy_of(pat):
+            import re as _re
+            sel = {k: v for k, v in ks.items() if _re.search(pat, k)}
+            w = sum(v["avg_us"] * v["dispatches"] for v in sel.values())
+            return (round(sum(v["mfma_busy"] * v["avg_us"] * v["dispatches"] for v in sel.values()) / w, 4) if w else None,
+                    {k: v["mfma_busy"] for k, v in sel.items()})
+        ch, ch_k = busy_of(r"gemm_x6m_kernel|gemm_lnch_kernel<\d+, [01]")
+        lp, lp_k = busy_of(r"chain_x6s_kernel")
+        roofline["mfma_busy"] = {"channel_gemms": ch, "logpsi_chain": lp, "per_kernel": {**ch_k, **lp_k},
+                                 "source": f"profiles/mfma_pmc.json ({mj.get('tag', '?')})",
+                                 "definition": "MFMA cycles / (dispatch cycles x 1024 SIMDs), time-weighted"}
     B_total = B * world
     value = B_total * args.steps / dt
     F_fwd = f_fwd(N, args.flux)
@@ -387,6 +416,10 @@ def main():
                 "kernels_ms_per_step": {k: round(v["ms_per_step"], 3)
                                         for k, v in kernels_of(rx["prof"], args.extra_steps).items()},
                 "energy": [round(rx["energy"].real, 5), round(rx["energy"].imag, 5)],
+                "walker_steps_per_sec": round(B * args.mcmc_steps / rx["t_mcmc"], 1) if rx["t_mcmc"] == rx["t_mcmc"] else None,
+                "walker_steps_per_sec_def": f"B x steps / t(mcmc_step call), mean of {args.extra_mcmc_calls} calls",
+                "mcmc_step_ms": round(1e3 * rx["t_mcmc"], 3) if rx["t_mcmc"] == rx["t_mcmc"] else None,
+                "local_energies_per_sec_el_only": round(B / rx["t_el"], 1) if rx["t_el"] == rx["t_el"] else None,
                 "model_tflops_step": round(B * (2 * n + 5 + args.mcmc_steps + 1) * f_fwd(n, fx)
                                            / rx["dt"] * args.extra_steps / 1e12, 2),
             }

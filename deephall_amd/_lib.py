@@ -73,6 +73,7 @@ EXPORTS = [
     "dh_profile_enable",
     "dh_profile_read",
     "dh_debug_f_offset",
+    "dh_debug_env_leaf",
     "dh_kfac_layout",
     "dh_kfac_workspace_bytes",
     "dh_kfac_vjp",
@@ -81,7 +82,7 @@ EXPORTS = [
 
 
 PROF_KINDS = ["gemm", "attention", "layernorm", "input", "det_value", "det_energy", "mcmc",
-              "gemm_ch", "attention_ch", "layernorm_ch", "input_ch"]
+              "gemm_ch", "attention_ch", "layernorm_ch", "input_ch", "layer1_ch"]
 
 
 class DhConfig(C.Structure):
@@ -162,6 +163,8 @@ def load(path: Path | str | None = None):
     lib.dh_debug_trunk.restype = i32
     lib.dh_debug_f_offset.argtypes = [vp, i32, i32]
     lib.dh_debug_f_offset.restype = sz
+    lib.dh_debug_env_leaf.argtypes = [vp, i32, i32, i32, vp, vp]
+    lib.dh_debug_env_leaf.restype = i32
     lib.dh_debug_gemm.argtypes = [i32, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp]
     lib.dh_debug_gemm.restype = i32
     lib.dh_debug_gemm_ln.argtypes = [i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp]

@@ -77,8 +77,9 @@ Work carve(const Dims& d, int nw, int C, void* base) {
 
 // Optional per-kernel HIP-event timing (bench.py reads it to compute the live roofline).
 enum ProfKind { PK_GEMM = 0, PK_ATTN, PK_LN, PK_INPUT, PK_DET_VALUE, PK_DET_ENERGY, PK_MCMC, PK_COUNT };
-// channel-mode (C > 1) launches of GEMM/attention/LayerNorm/input are recorded as kind + PK_CH
-constexpr int PK_CH = PK_COUNT, PK_TOTAL = PK_COUNT + 4;
+// channel-mode (C > 1) launches of GEMM/attention/LayerNorm/input are recorded as kind + PK_CH;
+// PK_L1CH: the local energy's layer 1 in one launch (gemm_lnch MODE 2)
+constexpr int PK_CH = PK_COUNT, PK_L1CH = PK_COUNT + 4, PK_TOTAL = PK_COUNT + 5;
 struct ProfRec {
   hipEvent_t a, b;
   int kind;
@@ -665,7 +666,8 @@ namespace {
 // One Psiformer pass over nw walkers with C channels; leaves orbital features in w.F.
 // geo_ready: w.geo already holds the walkers' geometry (written by the MCMC proposal); the
 // input kernel is then skipped when the geometry is all it would write.
-int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false) {
+int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStream_t s, bool geo_ready = false,
+              bool keep_h = false) {
   const Dims& d = h->d;
   const Params& P = h->p;
   const int rows = nw * d.N * C;
@@ -752,7 +754,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       launch_chain_x6(w.o, attn_in_chain ? P.UP : lp.WolP, x6_plane_rows(D), lp.bol, lp.ln1, lp.WmP, x6_plane_rows(D),
                       lp.bm, lp.ln2, last ? P.WorbP : P.layer[l + 1].WqkvP, x6_plane_rows(n3),
                       last ? P.borb : P.layer[l + 1].bqkv, n3, last ? w.F : w.qkv, last ? d.ld_orb : 3 * D, w.h, rows,
-                      feat, s, /*store_h=*/!last);  // the last layer's h is dead: only its orbitals are read
+                      feat, s, /*store_h=*/!last || keep_h);  // the last layer's h is dead: only its orbitals are read
       continue;
     }
     if (ln_fused) {
@@ -777,7 +779,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     if (lnch && l == 0 && fused && d.H == 4) {
       // layer 1 whole in one launch from the o~ rows (gemm_lnch MODE 2: LN1, Wm and tanh_ch in
       // coefficient space, the residual h1 from the same 32-deep rows, LN2)
-      PROF(PK_GEMM + PK_CH, 2.0 * R * DD * 3.0 * KO, f4 * (R * KO + R * DD));
+      PROF(PK_L1CH, 2.0 * R * DD * 3.0 * KO, f4 * (R * KO + R * DD));
       launch_gemm_lnch(d.N, w.o, P.UP, x6_plane_rows(D), lp.bol, lp.ln2, w.geo, w.h, nw * d.N, 2, s, P.W0, d.n_up, KO,
                        P.L1VP, P.L1BP);
       continue;
@@ -1614,7 +1616,14 @@ int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t
   const size_t need = h ? dh_workspace_bytes(h, B, op) : 0;
   if (int rc = check_common(h, x, B, ws, ws_bytes, need)) return rc;
   Work w = carve(h->d, B, op == 1 ? h->d.C : 1, ws);
-  return run_trunk(h, x, B, op == 1 ? h->d.C : 1, w, (hipStream_t)stream);
+  // keep_h: the chain form writes the last layer's h too (the production path skips it)
+  return run_trunk(h, x, B, op == 1 ? h->d.C : 1, w, (hipStream_t)stream, false, /*keep_h=*/true);
+}
+
+int dh_debug_env_leaf(const float* thph, int n, int M, int sq, float* out, void* stream) {
+  if (!thph || !out || n < 1 || M < 1) return fail(DH_EINVAL, "bad env_leaf probe args");
+  launch_env_leaf_probe(thph, n, M, sq, out, (hipStream_t)stream);
+  return check_launch();
 }
 
 size_t dh_debug_f_offset(const dh_handle* h, int B, int op) {

@@ -58,8 +58,11 @@ namespace dh {
 namespace {
 
 __device__ inline float ipow(float b, int e) { return e < 0 ? 0.f : (e == 0 ? 1.f : powf(b, (float)e)); }
-// integer power by squaring (det_value's envelope values: a few multiplies per power instead
-// of powf's log / exp; the same value to f32 rounding)
+// integer power by squaring (the envelope values and leaves: a few multiplies per power instead
+// of powf's log / exp).  Not powf's 1-ulp result: squaring doubles the relative error it
+// carries, so b^e is within about (e + popcount(e)) * 2^-24 relative (< 4e-6 at e = 57, C5's
+// largest exponent) against powf's ~6e-8; tests/test_gpu_kernels.py::test_env_leaf_powers
+// bounds both forms against float64 at M = 58 near the poles (dh_debug_env_leaf)
 __device__ inline float ipow_sq(float b, int e) {
   float r = 1.f;
   for (; e > 0; e >>= 1, b *= b)
@@ -382,7 +385,9 @@ __device__ inline double jastrow_pair(double r, double al, double cst, double* f
 // `per` floats): the serial parts (pivot search, log det, Jastrow reduction) then serve two
 // walkers per instruction.
 template <int MGV, bool HW = false>
-__global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* __restrict__ x,
+// x is not __restrict__: with the MCMC epilogue it is the same buffer as epi.x2, which the
+// epilogue writes (each thread reads its own walker's angles before that, behind a barrier)
+__global__ __launch_bounds__(64) void det_value_kernel(const float* __restrict__ Fp, int ldF, const float* x,
                                  const float* __restrict__ jas, const float* __restrict__ norm, float* __restrict__ logpsi,
                                  int N, int n_up, int M, int K, int nw, int per, McmcEpi epi) {
   static_assert(!HW || MGV == 0, "half-wave form: serial contraction only");
@@ -2396,5 +2401,23 @@ void launch_det_energy(const Dims& d, const float* F, const float* x, const floa
 }
 
 size_t det_energy_smem_bytes(const Dims& d) { return (size_t)det_layout(d.N, d.M, d.K, 4).total * sizeof(float); }
+
+namespace {
+// test hook kernel: env_leaf of n angle pairs, every harmonic p < M, in the production gauge
+__global__ void env_leaf_probe_kernel(const float* __restrict__ thph, int n, int M, int sq, float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * M) return;
+  const int i = t / M, p = t - i * M;
+  const float th = thph[2 * i], ph = thph[2 * i + 1];
+  const EnvLeaf L = env_leaf(th, ph, p, M, 1.f, true, env_gauge(cosf(th), M), sq != 0);
+  float* o = out + (size_t)t * 10;
+  o[0] = L.e0.re, o[1] = L.e0.im, o[2] = L.dth.re, o[3] = L.dth.im, o[4] = L.dph.re;
+  o[5] = L.dph.im, o[6] = L.lb.re, o[7] = L.lb.im, o[8] = L.d2th.re, o[9] = L.d2th.im;
+}
+}  // namespace
+
+void launch_env_leaf_probe(const float* thph, int n, int M, int sq, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(env_leaf_probe_kernel, dim3((n * M + 127) / 128), dim3(128), 0, s, thph, n, M, sq, out);
+}
 
 }  // namespace dh

@@ -231,6 +231,9 @@ bool det_precontract(const Dims& d);
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic);
 size_t det_energy_smem_bytes(const Dims& d);
+// test hook: env_leaf (e0, dth, dph, lb, d2th as re / im pairs: 10 floats) of n (theta, phi)
+// pairs for every harmonic p < M, norm 1, the production gauge; sq: powers by squaring
+void launch_env_leaf_probe(const float* thph, int n, int M, int sq, float* out, hipStream_t s);
 void launch_potential(const Dims& d, const float* x, float* pe, int nw, hipStream_t s);
 // mcmc.hip: accept/reject (mcmc.py:55-62).
 void launch_accept(const Dims& d, float* x, const float* x2, float* lp, const float* logpsi2, int32_t* n_acc,

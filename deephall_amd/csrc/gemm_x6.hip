@@ -2538,8 +2538,8 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     if (col0 < 3 * CH_BN) CHAIN_T(10 + 2 * (col0 / CH_BN));
 #if CHAIN_P3T
     {  // D[tile row][column]: reg q of acc[rb] = row 32 rb + (q & 3) + 8 (q >> 2) + 4 lh, column l32.
-      // Buffer stores: the tile's rows as the resource (rows past the batch fall outside it and
-      // are dropped), the row offset as soffset, one 32-bit lane offset (past the range off n3)
+      // Buffer stores: the tile's rows as the resource, one 32-bit lane offset (past the range off
+      // n3); full tiles put the row offset in soffset, the partial last tile in voffset
       const int c = col0 + 32 * wid + l32;
       const bool cok = c < a.n3;
       const float bv = cok ? a.b3[c] : 0.f;
@@ -2547,12 +2547,25 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
       const int nrow = min(CH_BM, rows - row0), ldb = a.ldy3 * 4;
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.Y3 + (size_t)row0 * a.ldy3, (short)0, nrow * ldb, 0x00020000);
       const int vo = cok ? 4 * lh * ldb + 4 * c : 0x7fffffff;
+      if (nrow == CH_BM) {  // full tile: the row offset in soffset (every row inside the resource)
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
+        for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[rb][q] + bv), rs, vo,
-                                                (32 * rb + (q & 3) + 8 * (q >> 2)) * ldb, 0);
+          for (int q = 0; q < 16; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[rb][q] + bv), rs, vo,
+                                                  (32 * rb + (q & 3) + 8 * (q >> 2)) * ldb, 0);
+        }
+      } else {  // the last, partial tile: the raw-buffer range check covers voffset only (not
+        // soffset), so the row goes into voffset and rows past the batch are out of range
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int r = 32 * rb + (q & 3) + 8 * (q >> 2) + 4 * lh;
+            const int v = (cok && r < nrow) ? 4 * c + r * ldb : 0x7fffffff;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[rb][q] + bv), rs, v, 0, 0);
+          }
+        }
       }
       if (col0 < 3 * CH_BN) CHAIN_T(11 + 2 * (col0 / CH_BN));
       continue;

@@ -315,7 +315,9 @@ int dh_kinetic_from_derivatives(const double* x, const double* grad, const doubl
  * FLOPs, algorithmic bytes} for kernel class k (returns the number of classes):
  *   0 GEMM  1 attention  2 LayerNorm  3 input  4 det (log psi)  5 det (energy)
  *   6 MCMC proposal/accept; 7-10 = classes 0-3 launched with 2N+5 channels
- *   (local energy).  Synchronises on the recorded events. */
+ *   (local energy); 11 = layer 1 of the local energy in one launch (gemm_lnch MODE 2:
+ *   LayerNorms, tanh and three 32-deep products).  out holds 4 * 12 doubles.
+ *   Synchronises on the recorded events. */
 int dh_profile_enable(dh_handle* h, int on);
 int dh_profile_read(dh_handle* h, double* out, int reset);
 
@@ -324,6 +326,11 @@ int dh_profile_read(dh_handle* h, double* out, int reset);
  * features at float offset dh_debug_f_offset). */
 int dh_debug_trunk(dh_handle* h, const float* x, int B, int op, void* ws, size_t ws_bytes, void* stream);
 size_t dh_debug_f_offset(const dh_handle* h, int B, int op);
+/* Test hook: the envelope leaves of det.hip's env_leaf (e0, d/dtheta, d/dphi / sin theta,
+ * Laplace-Beltrami, d2/dtheta2 as re / im pairs: 10 floats) of n (theta, phi) pairs thph[n][2]
+ * for every harmonic p < M (norm 1, the kernels' gauge kappa = env_gauge(cos theta)) into
+ * out[n][M][10]; sq = 1: integer powers by squaring (the production form), 0: powf. */
+int dh_debug_env_leaf(const float* thph, int n, int M, int sq, float* out, void* stream);
 /* Test hook: one launch of GEMM kernel variant `variant` (-1 = default):
  * Y = X W (+ bias on rows r % C == 0) (+ R).  X must hold round_up(rows, 256) rows.
  * variant >= 100 selects the NT kernels: W is then the TRANSPOSED weight Wt[n][k]

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import pytest
 import torch
 
@@ -250,3 +251,61 @@ def test_chain_x6_matches_separate_kernels(cuda, n3, rows):
     if n3:
         y = h2 @ W3.double() + b3.double()
         assert (Y_ch[:rows, :n3].double() - y).abs().max().item() < 2e-4 * max(1.0, y.abs().max().item())
+
+
+def _env_leaf_f64(th, ph, M):
+    """det.hip env_leaf in float64 (norm 1): [n][M][10] = e0, dth, dph, lb, d2th (re, im)."""
+    th = th.astype(np.float64)[:, None]
+    ph = ph.astype(np.float64)[:, None]
+    ct32 = np.cos(th.astype(np.float32)).astype(np.float32)
+    gauge = (np.float32(M - 1) * np.rint(np.float32(64.0) * ct32) * np.float32(1.0 / 128.0)).astype(np.float64)
+    p = np.arange(M)[None, :].astype(np.float64)
+    a, b = p, M - 1 - p
+    m = 0.5 * (a - b) - gauge
+    c, s = np.cos(0.5 * th), np.sin(0.5 * th)
+
+    def pw(x, e):
+        return np.where(e < 0, 0.0, np.power(x, np.maximum(e, 0)))
+
+    R = pw(c, a) * pw(s, b)
+    R1 = 0.5 * (b * pw(c, a + 1) * pw(s, b - 1) - a * pw(c, a - 1) * pw(s, b + 1))
+    R2 = 0.25 * (b * (b - 1) * pw(c, a + 2) * pw(s, b - 2) - b * (a + 1) * R - a * (b + 1) * R
+                 + a * (a - 1) * pw(c, a - 2) * pw(s, b + 2))
+    cph, sph = np.cos(m * ph), np.sin(m * ph)
+    st, ctd = np.sin(th), np.cos(th)
+    e0 = (R * cph, R * sph)
+    dth = (R1 * cph, R1 * sph)
+    d2 = (R2 * cph, R2 * sph)
+    dph = (-m * e0[1] / st, m * e0[0] / st)
+    k2, cot = m * m / (st * st), ctd / st
+    lb = (d2[0] - k2 * e0[0] + cot * dth[0], d2[1] - k2 * e0[1] + cot * dth[1])
+    return np.stack([e0[0], e0[1], dth[0], dth[1], dph[0], dph[1], lb[0], lb[1], d2[0], d2[1]], -1)
+
+
+@pytest.mark.parametrize("M", [16, 24, 58])
+def test_env_leaf_powers(cuda, M):
+    """The envelope leaves with integer powers by squaring (the production form of every
+    determinant kernel, det.hip ipow_sq) against float64, beside the powf form: squaring
+    carries about (e + popcount e) * 2^-24 relative error per power (e <= M - 1 = 57 at C5)
+    where powf carries ~1 ulp.  Near the poles the leaves' own f32 formulas (m / sin, m^2 /
+    sin^2, cot) dominate both forms' error (measured on the MI355X: max 1.8e-4 - 5.7e-4 of the
+    component's scale for both at M = 16 .. 58), so the gate is relative: the squaring form's
+    error distribution stays within that of powf (max 1.5x, p99 2x, plus 2e-6 of the scale)."""
+    lib = _lib.load()
+    g = np.random.default_rng(M)
+    th = np.concatenate([g.uniform(1e-3, 0.15, 32), np.pi - g.uniform(1e-3, 0.15, 32), g.uniform(0.15, np.pi - 0.15, 64)])
+    ph = g.uniform(0.0, 2 * np.pi, th.size)
+    thph = torch.tensor(np.stack([th, ph], -1).astype(np.float32), device="cuda")
+    th32, ph32 = thph[:, 0].cpu().numpy(), thph[:, 1].cpu().numpy()
+    ref = _env_leaf_f64(th32, ph32, M)
+    scale = np.abs(ref).max(axis=1, keepdims=True) + 1e-30  # per point and component, over p
+    errs = {}
+    for sq in (0, 1):
+        out = torch.empty(th.size * M * 10, device="cuda")
+        assert lib.dh_debug_env_leaf(_p(thph), th.size, M, sq, _p(out), _stream()) == 0
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().reshape(th.size, M, 10).astype(np.float64)
+        e = np.abs(got - ref) / scale
+        errs[sq] = (np.median(e), np.percentile(e, 99), e.max())
+    print(f"M={M}: env_leaf error / component scale (median, p99, max): powf {errs[0]}, squaring {errs[1]}")
+    assert errs[1][2] <= 1.5 * errs[0][2] + 2e-6 and errs[1][1] <= 2.0 * errs[0][1] + 2e-6, errs

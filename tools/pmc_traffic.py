@@ -38,8 +38,10 @@ def main(paths):
         tot_n += nf
     out["gemm_bytes_per_launch"] = tot_b / tot_n if tot_n else None
     # the local-energy channel GEMMs alone (split-bf16 kernel families, incl. the fused
-    # GEMM + channel LayerNorm of gemm_lnch.hip)
-    ch = [v for k, v in out["kernels"].items() if k.startswith(("gemm_x6q_kernel", "gemm_x6m_kernel", "gemm_lnch_kernel"))]
+    # GEMM + channel LayerNorm of gemm_lnch.hip; not its MODE 2, layer 1 whole: bench.py's
+    # roofline class is the 256-deep maps)
+    ch = [v for k, v in out["kernels"].items() if k.startswith(("gemm_x6q_kernel", "gemm_x6m_kernel", "gemm_lnch_kernel"))
+          and not re.match(r"gemm_lnch_kernel<\d+, 2", k)]
     n_ch = sum(v["launches"] for v in ch)
     out["channel_gemm_bytes_per_launch"] = (
         sum(v["bytes_per_launch"] * v["launches"] for v in ch) / n_ch if n_ch else None)
