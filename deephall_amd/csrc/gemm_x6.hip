@@ -35,12 +35,6 @@
 #ifndef X6M_BIAS1  // A/B knob: gemm_x6m's epilogue bias loads ahead of its stores (1) or between them (0)
 #define X6M_BIAS1 1
 #endif
-#ifndef CHAIN_ANT  // A/B knob: walkers per attention call in the layer-1 chain prologue (2 or 4)
-#define CHAIN_ANT 2
-#endif
-#ifndef CHAIN_APF  // A/B knob: layer 1's first weight fragments requested before (0) or after (1) the attention
-#define CHAIN_APF 0
-#endif
 #ifndef CHAIN_P3B  // A/B knob: P3 bias loads hoisted ahead of the stores (1) or between them (0)
 #define CHAIN_P3B 1
 #endif
@@ -2224,79 +2218,103 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
 
   // ---- P1 prologue: o rows -> planes (each element split once)
   if constexpr (NA > 0) {
-    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_KO == 32, "walker-aligned tiles, 4 heads x 2 wave groups");
-    constexpr int WPW = 48 / NA;  // walkers per wave
-    // walkers per attn_ofeat_core_g call (their LDS round trips overlap): CHAIN_ANT where it divides
-    constexpr int ANT = (CHAIN_ANT == 4 && WPW % 4 == 0) ? 4 : 2, PER = ANT * attn_feat_floats<NA>();
-    constexpr int NG = WPW / ANT, RG = attn_ofeat_regs<NA, ANT>();
-    static_assert(WPW % ANT == 0, "walker groups");
-    if (!CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0, KP1{});
-    float* qs = reinterpret_cast<float*>(smem) + wid * PER;
-    const int hd = wid & 3, wl0 = (wid >> 2) * WPW;  // head; first tile walker of this wave
-    const float* Mh = a.feat.Mqk + hd * kMqkStride;  // the head's score form (attn_feat_weights_g)
-    // the geometry of this wave's WPW walkers, staged once in wave-private LDS past the
-    // staging areas, and the head's score form in registers once
-    static_assert(WPW * NA <= 64 && CS_NW * (PER + 4 * WPW * NA) * 4 <= 3 * CS_PLANE, "geometry staging");
-    float4* gs = reinterpret_cast<float4*>(reinterpret_cast<float*>(smem) + CS_NW * PER) + wid * WPW * NA;
-    const int grow0 = row0 + wl0 * NA;  // first electron row of the wave's walkers
-    if (lane < WPW * NA)
-      gs[lane] = grow0 + lane < rows ? *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)(grow0 + lane))
-                                     : make_float4(0.f, 1.f, 0.f, 1.f);
-    float Mr[25];
+    // layer 1's attention in feature space for the tile's 96 / NA walkers and 4 heads, every
+    // phase spread over the whole workgroup (round 6; attn_val.h's arithmetic, operation for
+    // operation): (1) u_h,r = Mqk_h f~_r per (row, head), (2) per (walker, head, electron i)
+    // the scores f~_i . u_h,j and their softmax, (3) o~_h,i = sum_j A_ij f~_j into the planes'
+    // first 32 columns (head h at 8 h + a, slots 5..7 zero).  Staging lives in plane 0's
+    // columns 32.. (bytes 64.. of each 528-B row: 112 floats per row), which P1 never reads.
+    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_KO == 32, "walker-aligned tiles, 4 heads of 8 slots");
+    constexpr int WT = CH_BM / NA, NH = 4;  // walkers per tile, heads
+    static_assert(CH_BM * NH <= 512 && WT * NH * NA <= 512, "one thread per (row, head) and per (walker, head, electron)");
+    prefetch(a.Wp1, a.ldp1, 0, KP1{});
+    auto stg = [&](int k) __attribute__((always_inline)) {  // staging float k
+      return reinterpret_cast<float*>(smem + (size_t)(k / 112) * (LSP * 2) + 64 + (k % 112) * 4);
+    };
+    constexpr int F_ = 0, M_ = F_ + CH_BM * 5, U_ = M_ + NH * 25, A_ = U_ + CH_BM * NH * 5;  // staging layout
+    static_assert(A_ + WT * NH * NA * NA <= CH_BM * 112, "staging fits plane 0's free columns");
+    if (tid < CH_BM) {  // f~ of the tile's rows (rows past the batch: a valid dummy geometry)
+      const int gr = row0 + tid;
+      const float4 g = gr < rows ? *reinterpret_cast<const float4*>(a.feat.geo + 4 * (size_t)gr) : make_float4(0.f, 1.f, 0.f, 1.f);
+      *stg(F_ + 5 * tid) = g.y;
+      *stg(F_ + 5 * tid + 1) = g.x * g.w;
+      *stg(F_ + 5 * tid + 2) = g.x * g.z;
+      *stg(F_ + 5 * tid + 3) = (tid % NA < a.feat.n_up) ? 1.f : -1.f;
+      *stg(F_ + 5 * tid + 4) = 1.f;
+    } else if (tid < CH_BM + NH * 25) {
+      const int q = tid - CH_BM;
+      *stg(M_ + q) = a.feat.Mqk[(q / 25) * kMqkStride + q % 25];
+    }
+    lbar();
+    if (tid < CH_BM * NH) {  // (1) u_h,r = M_h f~_r
+      const int r = tid >> 2, hh = tid & 3;
+      float f[5];
 #pragma unroll
-    for (int q = 0; q < 25; ++q) Mr[q] = Mh[q];
-    __builtin_amdgcn_wave_barrier();
-    auto geo_at = [&](int row) __attribute__((always_inline)) { return gs[row - grow0]; };
-    // layer 1's o~ (attn_val.h attn_ofeat_core_g): 8 slots per (walker, electron) of this head
-    float ov[NG][RG];
+      for (int c = 0; c < 5; ++c) f[c] = *stg(F_ + 5 * r + c);
 #pragma unroll
-    for (int tg = 0; tg < NG; ++tg) {
-      const int b = row0 / NA + wl0 + tg * ANT;
-      if ((b + ANT) * NA <= rows) {
-        attn_ofeat_core_g<NA, ANT>(Mr, geo_at, b, a.feat.n_up, qs, lane, ov[tg]);
-      } else {  // the batch ends inside this group (last tile): whole walkers only, zeros past
-        float o1[attn_ofeat_regs<NA, 1>()];
+      for (int q = 0; q < 5; ++q) {
+        float u = 0.f;
 #pragma unroll
-        for (int u = 0; u < RG; ++u) ov[tg][u] = 0.f;
-#pragma unroll
-        for (int w = 0; w < ANT; ++w) {
-          if ((b + w + 1) * NA <= rows) {
-            attn_ofeat_core_g<NA, 1>(Mr, geo_at, b + w, a.feat.n_up, qs, lane, o1);
-            // walker w's values sit at p = 8 NA w + q of the ANT-walker layout
-#pragma unroll
-            for (int u = 0; u < RG; ++u) {
-              const int p = lane + 64 * u, q = p - 8 * NA * w;
-              float v = 0.f;
-#pragma unroll
-              for (int u1 = 0; u1 < attn_ofeat_regs<NA, 1>(); ++u1) {
-                const float x1 = __shfl(o1[u1], q & 63, 64);
-                if (q >= 0 && q < 8 * NA && (q >> 6) == u1) v = x1;
-              }
-              if (q >= 0 && q < 8 * NA) ov[tg][u] = v;
-            }
-          }
-        }
+        for (int c = 0; c < 5; ++c) u = fmaf(*stg(M_ + 25 * hh + 5 * q + c), f[c], u);
+        *stg(U_ + 5 * (NH * r + hh) + q) = u;
       }
     }
-    if (CHAIN_APF) prefetch(a.Wp1, a.ldp1, 0, KP1{});
-    lbar();  // the staging areas lie in the planes
+    lbar();
+    const int w = tid / (NH * NA), hh = (tid / NA) % NH, i = tid % NA;  // (walker, head, electron)
+    const bool act = tid < WT * NH * NA;
+    if (act) {  // (2) scores and softmax of row i
+      float fi[5], e[NA], m = -INFINITY;
 #pragma unroll
-    for (int tg = 0; tg < NG; ++tg)
+      for (int c = 0; c < 5; ++c) fi[c] = *stg(F_ + 5 * (w * NA + i) + c);
 #pragma unroll
-      for (int u = 0; u < RG; ++u) {  // one element: the three bf16 terms of split4
-        const int p = lane + 64 * u;
-        if (p < 8 * NA * ANT) {
-          const float x = ov[tg][u];
-          const uint32_t h2 = pk_bf16(x, 0.f);
-          const float rx = x - lo_f(h2);
-          const uint32_t m2 = pk_bf16(rx, 0.f);
-          const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
-          const int r = (wl0 + tg * ANT) * NA + (p >> 3), c = 8 * hd + (p & 7);
-          *reinterpret_cast<uint16_t*>(pl(0, r, c)) = (uint16_t)h2;
-          *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
-          *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
-        }
+      for (int j = 0; j < NA; ++j) {
+        float sc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) sc = fmaf(fi[q], *stg(U_ + 5 * (NH * (w * NA + j) + hh) + q), sc);
+        e[j] = sc;
+        m = fmaxf(m, sc);
       }
+      float ssum = 0.f;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        e[j] = expf(e[j] - m);
+        ssum += e[j];
+      }
+      const float inv = 1.f / ssum;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) *stg(A_ + NA * tid + j) = e[j] * inv;
+    }
+    lbar();
+    float ov[5];
+    if (act) {  // (3) o~ of row (w, i), head hh
+      float A[NA];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) A[j] = *stg(A_ + NA * tid + j);
+      const bool live = row0 + w * NA + i < rows;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        float acc1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) acc1 = fmaf(A[j], *stg(F_ + 5 * (w * NA + j) + q), acc1);
+        ov[q] = live ? acc1 : 0.f;
+      }
+    }
+    lbar();  // every staging read done: the o~ columns of the rows are written below
+    if (act) {
+      const int r = w * NA + i;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // one element: the three bf16 terms of split4
+        const float x = q < 5 ? ov[q] : 0.f;
+        const uint32_t h2 = pk_bf16(x, 0.f);
+        const float rx = x - lo_f(h2);
+        const uint32_t m2 = pk_bf16(rx, 0.f);
+        const uint32_t l2 = pk_bf16(rx - lo_f(m2), 0.f);
+        const int c = 8 * hh + q;
+        *reinterpret_cast<uint16_t*>(pl(0, r, c)) = (uint16_t)h2;
+        *reinterpret_cast<uint16_t*>(pl(1, r, c)) = (uint16_t)m2;
+        *reinterpret_cast<uint16_t*>(pl(2, r, c)) = (uint16_t)l2;
+      }
+    }
     lbar();
   } else {
     prefetch(a.Wp1, a.ldp1, 0, KP1{});

@@ -22,6 +22,11 @@ NAMES = ["prologue (o / X1 -> planes)", "P1 GEMM", "P1 bias + residual", "P1 Lay
          "P2 GEMM", "P2 h1 + tanh", "P2 LayerNorm", "P2 planes + h + barrier",
          "P3 pass 0 GEMM", "P3 pass 0 stores", "P3 pass 1 GEMM", "P3 pass 1 stores", "P3 pass 2 GEMM",
          "P3 pass 2 stores"]
+# layer 1 (round 6): o~ prologue, 32-deep P1, LN1 statistics + coefficient rows, P2 = r V, tanh, r B
+NAMES1 = ["prologue (o~ -> planes)", "P1 GEMM (o~ U, 32 deep)", "P1 bias + f W0", "LN1 stats + r rows",
+          "(none)", "P2: r V, tanh, += r B", "(none)", "P2 LayerNorm", "P2 planes + h + barrier",
+          "P3 pass 0 GEMM", "P3 pass 0 stores", "P3 pass 1 GEMM", "P3 pass 1 stores", "P3 pass 2 GEMM",
+          "P3 pass 2 stores"]
 
 
 def main():
@@ -50,9 +55,10 @@ def main():
         last = max(i for i in range(NS) if (t[:, i] > 0).all())
         tot = (t[:, last] - t[:, 0]).mean()
         print(f"== {name}: {len(t)} tiles, tile span {tot:.0f} cycles (stamps 0..{last})")
+        names = NAMES1 if slot == 1 else NAMES
         for i in range(last):
             d = (t[:, i + 1] - t[:, i]).mean()
-            print(f"   {NAMES[i]:30s} {d:9.0f} cycles  {100 * d / tot:5.1f} %")
+            print(f"   {names[i]:30s} {d:9.0f} cycles  {100 * d / tot:5.1f} %")
         spread = (t[:, 0] - t[:, 0].min()) 
         print(f"   tile start spread: median {np.median(spread):.0f}, max {spread.max():.0f} cycles")
 
