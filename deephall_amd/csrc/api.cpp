@@ -46,12 +46,20 @@ struct Work {
   size_t total_bytes;
 };
 
+// envelope first (det.hip): floats of S, FS, E2, Weff for nw walkers (each padded to 256 rows)
+size_t env_first_floats(const Dims& d, int nw) {
+  const size_t ne = (size_t)nw * d.N, r6 = (size_t)round_up((int)(6 * ne), 256), r1 = (size_t)round_up((int)ne, 256);
+  return align64(r6 * 256) + align64(r6 * d.ld_orb) + align64(r1 * env_first_k(d)) + align64(r1 * 256 * 2 * d.N);
+}
+
 Work carve(const Dims& d, int nw, int C, void* base) {
   const int rows = nw * d.N * C;
   // + CH_BM rows: the channel chain's electron-aligned 96-row tiles read past the last row
   const size_t rp = (size_t)round_up(std::max(rows, 1) + 96, kWalkerRowPad);
   const size_t nh = align64(rp * d.D);
-  const size_t nqkv = align64(rp * (size_t)std::max(3 * d.D, d.ld_orb));
+  size_t nqkv = align64(rp * (size_t)std::max(3 * d.D, d.ld_orb));
+  if (C > 1 && env_first(d))  // no F over the channel rows: S, FS, E2, Weff share the q|k|v buffer
+    nqkv = align64(std::max(rp * (size_t)(3 * d.D), env_first_floats(d, nw)));
   Work w{};
   size_t off = 0;
   auto take = [&](size_t n) {
@@ -134,6 +142,8 @@ struct dh_handle {
   float* ofw = nullptr;    // layer 1's feature-space output map U^T [256 pad][KO] (launch_ofeat_weight)
   uint16_t* ofp = nullptr;  // its split-bf16 planes [3][x6_plane_rows(D)][KO]
   float* l1w = nullptr;     // layer 1's coefficient-space maps B^T, V^T (launch_l1_basis)
+  float* w2t = nullptr;     // envelope first: W2T [256 2N][KE] (launch_env_w2)
+  uint16_t* w2p = nullptr;  // its planes
   uint16_t* l1p = nullptr;  // their planes
   int gemm_mode = DH_GEMM_X6_ALL;
   std::vector<float> norm_host;
@@ -374,6 +384,8 @@ void dh_destroy(dh_handle* h) {
   if (h->ofw) (void)hipFree(h->ofw);
   if (h->ofp) (void)hipFree(h->ofp);
   if (h->l1w) (void)hipFree(h->l1w);
+  if (h->w2t) (void)hipFree(h->w2t);
+  if (h->w2p) (void)hipFree(h->w2p);
   if (h->l1p) (void)hipFree(h->l1p);
   if (h->ref) (void)hipFree(h->ref);
   if (h->wb) (void)hipFree(h->wb);
@@ -509,6 +521,15 @@ int derive_weights(dh_handle* h, hipStream_t st) {
     }
     launch_split_planes(h->p.WorbT, D, d.orb_cols, D, w, st);
     h->p.WorbP = w;
+    if (env_first(d)) {  // envelope first (C4 / C5): the envelope-coefficient map of Worb
+      const int KE = env_first_k(d), n2 = 256 * 2 * d.N;
+      if (!h->w2t) HIP_TRY(hipMalloc(&h->w2t, (size_t)n2 * KE * sizeof(float)));
+      if (!h->w2p) HIP_TRY(hipMalloc(&h->w2p, (size_t)3 * x6_plane_rows(n2) * KE * sizeof(uint16_t)));
+      launch_env_w2(d, h->p.Worb, h->w2t, st);
+      launch_split_planes(h->w2t, KE, n2, KE, h->w2p, st);
+      h->p.W2T = h->w2t;
+      h->p.W2P = h->w2p;
+    }
     // backward planes: the untransposed W [K = D][n] read as a transposed weight with D
     // output rows and contraction length n (dX = dY W^T)
     const int pr = x6_plane_rows(D);
@@ -818,7 +839,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       launch_layernorm(d, nullptr, w.o, lp.ln2, w.geo, w.h, nw, C, 1, s);
     }
   }
-  if (!chain || d.L == 0)
+  // (the envelope-first local energy maps only six special rows per electron, det.hip)
+  if ((!chain || d.L == 0) && !(C > 1 && env_first(d)))
     gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }
@@ -948,6 +970,28 @@ int dh_local_energy(dh_handle* h, const float* x, int B, float* e_l, float* obs,
     Work w = carve(d, nw, d.C, ws);
     const float* xc = x + (size_t)b0 * d.N * 2;
     if (int rc = run_trunk(h, xc, nw, d.C, w, s)) return rc;
+    if (env_first(d)) {
+      // envelope first (det.hip): PhiC straight from h, then the determinant algebra
+      const size_t ne = (size_t)nw * d.N, r6 = (size_t)round_up((int)(6 * ne), 256);
+      const size_t r1 = (size_t)round_up((int)ne, 256);
+      float* S = w.qkv;
+      float* FS = S + align64(r6 * 256);
+      float* E2 = FS + align64(r6 * d.ld_orb);
+      float* Weff = E2 + align64(r1 * env_first_k(d));
+      {
+        PROF(PK_GEMM + PK_CH, 2.0 * 6 * ne * d.D * d.orb_cols + 2.0 * ne * env_first_k(d) * 256 * 2 * d.N +
+                                  2.0 * ne * d.C * 256 * 2 * d.N,
+             4.0 * ne * (7.0 * 256 + 6.0 * d.ld_orb + env_first_k(d) + 2.0 * 256 * 2 * d.N + d.C * 256));
+        launch_env_first(d, w.h, w.geo, xc, h->norm, h->p.WorbT, h->p.borb, h->p.WorbP, h->p.W2T, h->p.W2P,
+                         h->gemm_mode != DH_GEMM_F32, nw, S, FS, E2, Weff, w.o, s);
+      }
+      {
+        PROF(PK_DET_ENERGY, 0.0, 8.0 * nw * d.C * d.N * d.N);
+        launch_det_energy_pc(d, xc, w.geo, h->p.jastrow, h->norm, e_l + 2 * (size_t)b0, obs + 8 * (size_t)b0, nw, s, w.o);
+      }
+      if (int rc = check_launch()) return rc;
+      continue;
+    }
     {
       PROF(PK_DET_ENERGY, 0.0, 4.0 * nw * d.N * d.C * d.ld_orb);
       // the trunk's o buffer (rows x D floats) is free here and holds nw K C N N complex when 2 K N <= D

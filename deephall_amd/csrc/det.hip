@@ -2420,4 +2420,298 @@ void launch_env_leaf_probe(const float* thph, int n, int M, int sq, float* out, 
   hipLaunchKernelGGL(env_leaf_probe_kernel, dim3((n * M + 127) / 128), dim3(128), 0, s, thph, n, M, sq, out);
 }
 
+
+
+// ------------------------------------------------------------------ envelope first (round 6)
+// C4 / C5 (one spin block, one determinant, N > 8): every entry the determinant algebra reads is
+// Phi_c[i][j] = sum_m F_c[i](m, j) e_m(x_i) + (own-electron / value-row leaf terms), with
+// F_c[i] = h_c[i] W.  By associativity the e0 part is h_c[i] . Weff_i[:, j] with
+// Weff_i = sum_m e_m(x_i) W[:, (m, j)] (256 x N complex per electron), so the 2 M N-column
+// orbital map over all C channel rows (C5: 4.4 TFLOP per step, F = 34 GB written and read back)
+// is replaced by
+//   (1) Weff = E2 W2 — one GEMM over the electrons (rows: the envelope coefficients
+//       (Re e_m | Im e_m) of each electron, K = 2 M padded to 32; columns (j, re / im, k));
+//   (2) F of six special rows per electron only — the value row (with the bias), the two own
+//       tangent rows, and the three flow rows hu_k = sum_t alpha_kt h_t (the tangent rows'
+//       W_k terms of env_stream_kernel summed over t before the map instead of after);
+//   (3) env_phi_kernel: h_c . Weff on the matrix cores (exact f32), the special rows'
+//       leaf contractions (e0, d/dtheta, d/dphi, LB, flow2_k, W_k) from their F, and the
+//       same assembly as env_stream_kernel -> PhiC for det_energy_kernel<0, true>.
+// blocks.py:64-68 / psiformer.py:74 (the envelope sum), hamiltonian.py (the channels).
+bool env_first(const Dims& d) {
+  return d.K == 1 && d.NB == 1 && (d.N == 10 || d.N == 20) && d.D == 256 && 2 * d.M <= 128 && det_precontract(d);
+}
+int env_first_k(const Dims& d) { return round_up(2 * d.M, 32); }
+
+namespace {
+
+// S rows [e][6][256]: h_0, h_(1+2i), h_(2+2i), hu_0..2 (hu_k = sum_t alpha_kt h_t); the T
+// tangent rows are loaded in one unrolled burst
+template <int N>
+__global__ __launch_bounds__(256) void srows_kernel(const float* __restrict__ h, const float* __restrict__ geo,
+                                                    float* __restrict__ S) {
+  const int e = blockIdx.x, b = e / N, i = e - (e / N) * N, k = threadIdx.x;
+  constexpr int T = 2 * N, C = 2 * N + 5;
+  const float* hr = h + (size_t)e * C * 256 + k;
+  float* sr = S + (size_t)e * 6 * 256 + k;
+  sr[0] = hr[0];
+  sr[256] = hr[(size_t)(1 + 2 * i) * 256];
+  sr[512] = hr[(size_t)(2 + 2 * i) * 256];
+  float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const float4 q = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + (t >> 1)));  // st ct sp cp
+    const float ht = hr[(size_t)(1 + t) * 256];
+    if ((t & 1) == 0) {
+      u0 = fmaf(-q.z, ht, u0);
+      u1 = fmaf(q.w, ht, u1);
+    } else {
+      u0 = fmaf(-(q.y * q.w), ht, u0);
+      u1 = fmaf(-(q.y * q.z), ht, u1);
+      u2 = fmaf(q.x, ht, u2);
+    }
+  }
+  sr[768] = u0;
+  sr[1024] = u1;
+  sr[1280] = u2;
+}
+
+// E2 [e][KE]: (Re e_m | Im e_m | 0 ...) of electron e, the leaves' own e0 (norm, gauge)
+__global__ void env_coef_kernel(const float* __restrict__ x, const float* __restrict__ geo,
+                                const float* __restrict__ norm, float* __restrict__ E2, int ne, int M, int KE) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ne * KE) return;
+  const int e = t / KE, q = t - (t / KE) * KE;
+  float v = 0.f;
+  if (q < 2 * M) {
+    const int p = q < M ? q : q - M;
+    const float gauge = env_gauge(geo[4 * (size_t)e + 1], M);
+    const EnvLeaf L = env_leaf(x[2 * (size_t)e], x[2 * (size_t)e + 1], p, M, norm[p], false, gauge, DET_LEAF_SQ);
+    v = q < M ? L.e0.re : L.e0.im;
+  }
+  E2[t] = v;
+}
+
+// W2T [n = (2 j + part) 256 + k][KE]: Weff_re[k][j] = sum_m Wre e_re - Wim e_im, Weff_im = Wre e_im + Wim e_re
+__global__ void env_w2_kernel(const float* __restrict__ Worb, int ldw, int M, int N, int D, int KE,
+                              float* __restrict__ W2T) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= D * 2 * N * KE) return;
+  const int n = t / KE, q = t - (t / KE) * KE;
+  const int jp = n / D, k = n - (n / D) * D, j = jp >> 1, part = jp & 1;  // Weff laid out [jp][k]
+  float v = 0.f;
+  if (q < 2 * M) {
+    const int m = q < M ? q : q - M, qim = q >= M, MN = M * N;
+    const float wre = Worb[(size_t)k * ldw + m * N + j], wim = Worb[(size_t)k * ldw + MN + m * N + j];
+    v = part == 0 ? (qim ? -wim : wre) : (qim ? wre : wim);
+  }
+  W2T[t] = v;
+}
+
+typedef float f4e __attribute__((ext_vector_type(4)));
+
+// One 256-thread workgroup per electron, one burst of loads up front: the six special F rows
+// (LDS-DMA) and the MFMA operands of h_c . Weff
+// (v_mfma_f32_16x16x4_f32, exact f32) straight from global memory.  The product is split over
+// K: wave w takes k in [64 w, 64 w + 64), lane (r, g) of a 16 x 16 tile row / column r and the
+// 16 contiguous k at 64 w + 16 g (4 float4 per operand tile; Weff is laid out [jp][k] for
+// that, env_w2_kernel).  The four per-wave partial tiles are summed in a fixed order at the
+// assembly (bitwise repeatable), in LDS that the special rows free once their 14 leaf
+// contractions per orbital are done.
+template <int N>
+__global__ __launch_bounds__(256) void env_phi_kernel(const float* __restrict__ h, const float* __restrict__ Weff,
+                                                     const float* __restrict__ FS, int ldF,
+                                                     const float* __restrict__ x, const float* __restrict__ geo_g,
+                                                     const float* __restrict__ norm, float* __restrict__ PhiC, int M) {
+  constexpr int T = 2 * N, C = 2 * N + 5, J2 = 2 * N, JP = 48, NE = 14;
+  constexpr int TR = (C + 15) / 16, TC = (J2 + 15) / 16;
+  static_assert(TR <= 3 && TC <= 3, "tile sizes");
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int e = blockIdx.x, b = e / N, i = e - (e / N) * N, M1 = M + 1, MN = M * N, RW = 2 * MN;
+  float* fsl = sm;                                  // [6][RW] the special rows; later [4][48][JP] partials
+  cf* wt = reinterpret_cast<cf*>(sm + (6 * RW > 4 * 48 * JP ? 6 * RW : 4 * 48 * JP));  // [10][M + 1]
+  cf* ext = wt + 10 * M1;                           // [NE][N]
+  // ---- the load burst: the special rows by LDS-DMA (global_load_lds_dwordx4, 1-KiB pieces,
+  // no VGPRs), then the MFMA operands into registers
+  {
+    const int RB = RW * 4, PR = (RB + 1023) / 1024;  // bytes / pieces per row
+    const uint32_t base = (uint32_t)(size_t)((__attribute__((address_space(3))) char*)fsl);
+    for (int q = wv; q < 6 * PR; q += 4) {
+      const int r = q / PR, piece = q - (q / PR) * PR, byte = piece * 1024 + lane * 16;
+      const char* src = reinterpret_cast<const char*>(FS + ((size_t)e * 6 + r) * ldF) + byte;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(base + (uint32_t)(r * RB + piece * 1024));
+      if (byte < RB) {
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(dst)
+                     : "memory");
+      }
+    }
+  }
+  const int r16 = lane & 15, kq = lane >> 4, k0 = 64 * wv + 16 * kq;
+  float4 av[TR][4], bv[TC][4];
+#pragma unroll
+  for (int t = 0; t < TR; ++t) {
+    const int row = 16 * t + r16;
+    const float* ap = h + ((size_t)e * C + (row < C ? row : 0)) * 256 + k0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) av[t][q] = *reinterpret_cast<const float4*>(ap + 4 * q);
+  }
+#pragma unroll
+  for (int t = 0; t < TC; ++t) {
+    const int col = 16 * t + r16;
+    const float* bp = Weff + ((size_t)e * J2 + (col < J2 ? col : 0)) * 256 + k0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bv[t][q] = *reinterpret_cast<const float4*>(bp + 4 * q);
+  }
+  // ---- the leaves while the loads are in flight
+  {
+    const float4 g4 = *reinterpret_cast<const float4*>(geo_g + 4 * (size_t)e);
+    const float th = x[2 * (size_t)e], ph = x[2 * (size_t)e + 1];
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const float gauge = env_gauge(ct, M);
+    const float phh[3] = {-sp, cp, 0.f};
+    const float thh[3] = {ct * cp, ct * sp, -st};
+    for (int p = tid; p < M; p += 256) {
+      const EnvLeaf L = env_leaf(th, ph, p, M, norm[p], true, gauge, DET_LEAF_SQ);
+      wt[p] = L.e0;
+      wt[M1 + p] = L.dth;
+      wt[2 * M1 + p] = L.dph;
+      wt[3 * M1 + p] = L.lb;
+      const float mf = (float)p - 0.5f * (float)(M - 1) - gauge;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        wt[(4 + k) * M1 + p] = cf{phh[k] * L.dth.re - thh[k] * L.dph.re, phh[k] * L.dth.im - thh[k] * L.dph.im};
+        wt[(7 + k) * M1 + p] = env_flow2(L.e0, L.dth, L.d2th, mf, st, ct, sp, cp, k);
+      }
+    }
+  }
+  // ---- the partial h_c . Weff tiles of this wave's k range
+  f4e acc[TR][TC];
+#pragma unroll
+  for (int t = 0; t < TR; ++t)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      acc[t][c] = f4e{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][q].x, bv[c][q].x, acc[t][c], 0, 0, 0);
+        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][q].y, bv[c][q].y, acc[t][c], 0, 0, 0);
+        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][q].z, bv[c][q].z, acc[t][c], 0, 0, 0);
+        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][q].w, bv[c][q].w, acc[t][c], 0, 0, 0);
+      }
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA pieces
+  __syncthreads();
+  // ---- the special rows' leaf contractions (row s of fsl: 0 value, 1 / 2 own tangents 2 i /
+  // 2 i + 1, 3..5 the flow rows): sums over the M harmonics
+  for (int q = tid; q < NE * N; q += 256) {
+    const int s = q / N, j = q - (q / N) * N;
+    // (row, leaf) of sum s: E0 DTH DPH LB SF0 SF1 SF2 of the value row; E0, DTH of own 2 i;
+    // E0, DPH of own 2 i + 1; W0, W1, W2 of the flow rows
+    const int row = s < 7 ? 0 : (s < 9 ? 1 : (s < 11 ? 2 : s - 8));
+    const int leaf = s == 0 ? 0 : (s < 4 ? s : (s < 7 ? s + 3 : (s == 7 ? 0 : (s == 8 ? 1 : (s == 9 ? 0 : (s == 10 ? 2 : s - 7))))));
+    const float* r = fsl + row * RW + j;
+    const cf* wl = wt + leaf * M1;
+    cf a0{0.f, 0.f}, a1{0.f, 0.f};
+    int m = 0;
+    for (; m + 1 < M; m += 2) {
+      cfma(a0, cf{r[m * N], r[MN + m * N]}, wl[m]);
+      cfma(a1, cf{r[(m + 1) * N], r[MN + (m + 1) * N]}, wl[m + 1]);
+    }
+    if (m < M) cfma(a0, cf{r[m * N], r[MN + m * N]}, wl[m]);
+    ext[s * N + j] = a0 + a1;
+  }
+  __syncthreads();
+  float* part = fsl;  // [4][48][JP]
+#pragma unroll
+  for (int t = 0; t < TR; ++t)
+#pragma unroll
+    for (int c = 0; c < TC; ++c)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) part[(wv * 48 + 16 * t + 4 * kq + v) * JP + 16 * c + r16] = acc[t][c][v];
+  __syncthreads();
+  // ---- assembly (env_stream_kernel's): PhiC[b][0][c][i][j]
+  for (int q = tid; q < C * N; q += 256) {
+    const int c = q / N, j = q - (q / N) * N;
+    cf r{0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      r.re += part[(w * 48 + c) * JP + 2 * j];
+      r.im += part[(w * 48 + c) * JP + 2 * j + 1];
+    }
+    cf v;
+    if (c == 0) {
+      v = ext[j];
+    } else if (c <= T) {
+      const int t = c - 1;
+      if ((t >> 1) == i)
+        v = (t & 1) ? ext[9 * N + j] + ext[2 * N + j] : ext[7 * N + j] + ext[1 * N + j];
+      else
+        v = r;
+    } else if (c == T + 1) {
+      v = r + ext[3 * N + j] + 2.f * (ext[8 * N + j] + ext[10 * N + j]);
+    } else {
+      const int k = c - T - 2;
+      v = r + ext[(4 + k) * N + j] + 2.f * ext[(11 + k) * N + j];
+    }
+    float* o = PhiC + 2 * (((size_t)b * C + c) * N * N + (size_t)i * N + j);
+    o[0] = v.re;
+    o[1] = v.im;
+  }
+}
+
+}  // namespace
+
+size_t env_phi_smem_bytes(const Dims& d) {
+  return (size_t)std::max(6 * 2 * d.M * d.N, 4 * 48 * 48) * sizeof(float) +
+         (size_t)(10 * (d.M + 1) + 14 * d.N) * sizeof(cf);
+}
+
+void launch_env_first(const Dims& d, const float* h, const float* geo, const float* x, const float* norm,
+                      const float* WorbT, const float* borb, const uint16_t* WorbP, const float* W2T,
+                      const uint16_t* W2P, bool x6, int nw, float* S, float* FS, float* E2, float* Weff, float* phic,
+                      hipStream_t s) {
+  const int ne = nw * d.N, KE = env_first_k(d), J2 = 2 * d.N;
+  if (d.N == 10)
+    hipLaunchKernelGGL(srows_kernel<10>, dim3(ne), dim3(256), 0, s, h, geo, S);
+  else  // env_first: N = 10 or 20
+    hipLaunchKernelGGL(srows_kernel<20>, dim3(ne), dim3(256), 0, s, h, geo, S);
+  hipLaunchKernelGGL(env_coef_kernel, dim3((ne * KE + 255) / 256), dim3(256), 0, s, x, geo, norm, E2, ne, d.M, KE);
+  if (x6) {  // split-bf16 (the default); exact-f32 NT GEMMs in DH_GEMM_F32
+    launch_gemm_x6(S, 256, WorbP, x6_plane_rows(d.orb_cols), borb, nullptr, 0, FS, d.ld_orb, 6 * ne, d.orb_cols, 256,
+                   6, s);
+    launch_gemm_x6(E2, KE, W2P, x6_plane_rows(256 * J2), nullptr, nullptr, 0, Weff, 256 * J2, ne, 256 * J2, KE, 1, s);
+  } else {
+    launch_gemm_nt(S, 256, WorbT, 256, borb, nullptr, 0, FS, d.ld_orb, 6 * ne, d.orb_cols, 256, 6, s);
+    launch_gemm_nt(E2, KE, W2T, KE, nullptr, nullptr, 0, Weff, 256 * J2, ne, 256 * J2, KE, 1, s);
+  }
+  const size_t smem = env_phi_smem_bytes(d);
+  auto go = [&](auto kern) {
+    ensure_smem(kern, smem);
+    hipLaunchKernelGGL(kern, dim3(ne), dim3(256), smem, s, h, Weff, FS, d.ld_orb, x, geo, norm, phic, d.M);
+  };
+  switch (d.N) {
+    case 10: go(env_phi_kernel<10>); break;
+    default: go(env_phi_kernel<20>); break;  // env_first: N = 10 or 20
+  }
+}
+
+void launch_env_w2(const Dims& d, const float* Worb, float* W2T, hipStream_t s) {
+  const int n = 256 * 2 * d.N * env_first_k(d);
+  hipLaunchKernelGGL(env_w2_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Worb, d.ld_orb, d.M, d.N, 256,
+                     env_first_k(d), W2T);
+}
+
+void launch_det_energy_pc(const Dims& d, const float* x, const float* geo, const float* jastrow, const float* norm,
+                          float* e_l, float* obs, int nw, hipStream_t s, const float* phic) {
+  const DetSmem L = det_layout(d.N, d.M, d.K, 4, true);
+  const size_t bytes = (size_t)L.total * sizeof(float);
+  ensure_smem(det_energy_kernel<0, true>, bytes);
+  hipLaunchKernelGGL((det_energy_kernel<0, true>), dim3(nw), dim3(256), bytes, s, nullptr, d.ld_orb, x, geo, jastrow,
+                     norm, e_l, obs, d.N, d.n_up, d.M, d.K, d.Q, d.r, d.lambda, d.interaction, phic);
+}
+
 }  // namespace dh

@@ -53,6 +53,8 @@ struct Params {
   const uint16_t* UP;
   // layer 1 in coefficient space (gemm_lnch MODE 2, H = 4): planes of V^T and B^T [3][ldp][32]
   const uint16_t *L1VP, *L1BP;
+  const float* W2T;     // envelope first (env_first): W2T [256 2N][KE] and its planes
+  const uint16_t* W2P;
 };
 // Layer 1's attention output in feature space (attention.hip feat2, the chain prologue): per
 // row o~ [ofeat_k] = per head h the five sums o~_h[a] = sum_j A_ij f~_j[a] (f~ = (z, x, y,
@@ -231,6 +233,22 @@ bool det_precontract(const Dims& d);
 void launch_det_energy(const Dims& d, const float* F, const float* x, const float* geo, const float* jastrow,
                        const float* norm, float* e_l, float* obs, int nw, hipStream_t s, float* phic);
 size_t det_energy_smem_bytes(const Dims& d);
+// envelope first (round 6, C4 / C5: one spin block, one determinant, N > 8; det.hip): the
+// channel matrices PhiC from h directly — Weff = E2 W2 per electron, F of six special rows per
+// electron, env_phi_kernel — instead of the full orbital map F and env_stream / env_contract
+bool env_first(const Dims& d);
+int env_first_k(const Dims& d);  // KE: the envelope-coefficient row length (2 M padded to 32)
+// W2T [256 * 2N][KE] from the packed Worb (launch_split_planes makes its planes)
+void launch_env_w2(const Dims& d, const float* Worb, float* W2T, hipStream_t s);
+// S [round_up(6 ne, 256)][256], FS [round_up(6 ne, 256)][ld_orb], E2 [round_up(ne, 256)][KE],
+// Weff [round_up(ne, 256)][256 * 2N] (ne = nw N): workspace; phic [nw][C][N][N] complex
+void launch_env_first(const Dims& d, const float* h, const float* geo, const float* x, const float* norm,
+                      const float* WorbT, const float* borb, const uint16_t* WorbP, const float* W2T,
+                      const uint16_t* W2P, bool x6, int nw, float* S, float* FS, float* E2, float* Weff, float* phic,
+                      hipStream_t s);
+// det_energy_kernel<0, true> alone on precontracted channel matrices
+void launch_det_energy_pc(const Dims& d, const float* x, const float* geo, const float* jastrow, const float* norm,
+                          float* e_l, float* obs, int nw, hipStream_t s, const float* phic);
 // test hook: env_leaf (e0, dth, dph, lb, d2th as re / im pairs: 10 floats) of n (theta, phi)
 // pairs for every harmonic p < M, norm 1, the production gauge; sq: powers by squaring
 void launch_env_leaf_probe(const float* thph, int n, int M, int sq, float* out, hipStream_t s);
