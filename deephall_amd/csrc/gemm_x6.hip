@@ -2001,7 +2001,10 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
     const int nblk = gridDim.x, q = nblk / 8, r8 = nblk % 8, xcd = bid % 8, slot = bid / 8;
     bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + slot;
   }
-  const int row0 = bid * CH_BM, rows = a.rows;
+  // rows per tile: 96, or with the attention in the prologue the whole walkers in 96 (N = 10:
+  // 9 walkers = 90 rows; the last 96 - TRW rows of the tile are computed and never stored)
+  constexpr int TRW = NA > 0 ? (CH_BM / NA) * NA : CH_BM;
+  const int row0 = bid * TRW, rows = min(a.rows, row0 + TRW);
   // every barrier of this kernel orders LDS only (planes, partial sums, staging); no wave reads
   // global memory another wave of the launch wrote, so the VMEM queue (weight prefetch, h / Y3
   // stores) may stay in flight across it
@@ -2218,13 +2221,13 @@ __global__ __launch_bounds__(512) void chain_x6s_kernel(ChainArgs a) {
 
   // ---- P1 prologue: o rows -> planes (each element split once)
   if constexpr (NA > 0) {
-    // layer 1's attention in feature space for the tile's 96 / NA walkers and 4 heads, every
+    // layer 1's attention in feature space for the tile's TRW / NA walkers and 4 heads, every
     // phase spread over the whole workgroup (round 6; attn_val.h's arithmetic, operation for
     // operation): (1) u_h,r = Mqk_h f~_r per (row, head), (2) per (walker, head, electron i)
     // the scores f~_i . u_h,j and their softmax, (3) o~_h,i = sum_j A_ij f~_j into the planes'
     // first 32 columns (head h at 8 h + a, slots 5..7 zero).  Staging lives in plane 0's
     // columns 32.. (bytes 64.. of each 528-B row: 112 floats per row), which P1 never reads.
-    static_assert(CH_BM % NA == 0 && CS_NW == 8 && CH_KO == 32, "walker-aligned tiles, 4 heads of 8 slots");
+    static_assert(CS_NW == 8 && CH_KO == 32, "4 heads of 8 slots");
     constexpr int WT = CH_BM / NA, NH = 4;  // walkers per tile, heads
     static_assert(CH_BM * NH <= 512 && WT * NH * NA <= 512, "one thread per (row, head) and per (walker, head, electron)");
     prefetch(a.Wp1, a.ldp1, 0, KP1{});
@@ -2982,17 +2985,19 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
       case 3: k = chain_x6s_kernel<3>; break;
       case 4: k = chain_x6s_kernel<4>; break;
       case 6: k = chain_x6s_kernel<6>; break;
-      default: k = chain_x6s_kernel<8>; break;
+      case 8: k = chain_x6s_kernel<8>; break;
+      default: k = chain_x6s_kernel<10>; break;
     }
   }
+  const int trw = feat.W0qkv ? (CH_BM / feat.N) * feat.N : CH_BM;  // the kernel's TRW
   ensure_smem(k, CS_SMEM);
-  hipLaunchKernelGGL(k, dim3((rows + CH_BM - 1) / CH_BM), dim3(512), CS_SMEM, s, a);
+  hipLaunchKernelGGL(k, dim3((rows + trw - 1) / trw), dim3(512), CS_SMEM, s, a);
 }
 
 // Layer 1's attention inside the chain prologue (chain_x6s_kernel<N>): walker-aligned 96-row
 // tiles, 4 heads of 64 (one per wave pair)
 bool chain_attn_supported(int N, int H, int dh) {
-  return H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8);
+  return H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8 || N == 10);
 }
 
 }  // namespace dh

@@ -6,9 +6,10 @@ o Wol = o~ (Wv~ Wol) = o~ U contracts over 8 H = 32 instead of 256 (psiformer.py
 chain kernel's prologue (log psi, rows < 65536) and attention_feat2_kernel + gemm_lnch (the
 local energy) take that form; the log-psi path for larger batches still forms o (256 wide,
 attention_val_kernel) and contracts it with Wol.  Both routes must agree to f32 rounding on the
-same walkers (distribution of the relative difference: median, p99, max): the first 1000 walkers of a batch past 65536 rows (the o route) against the same
-1000 walkers alone (the o~ route, with a partial last 96-row tile), for N = 6 (C2), N = 3 and
-the two-spin N = 4; and the local energy of the o~ route against the float64 oracle lives in
+same walkers (distribution of the relative difference: median, p99, max): the first 1000
+walkers of a batch past 65536 rows (the o route) against the same 1000 walkers alone (the o~
+route, with a partial last tile), for N = 6 (C2), N = 3, the two-spin N = 4 and N = 10 (C4:
+90-row tiles of 9 whole walkers); and the local energy of the o~ route against the float64 oracle lives in
 test_gpu_parity.py / test_gpu_floor.py."""
 
 from __future__ import annotations
@@ -24,7 +25,7 @@ from deephall_amd.train import init_guess
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nspins,flux", [((6, 0), 15), ((3, 0), 2), ((2, 2), 3)])
+@pytest.mark.parametrize("nspins,flux", [((6, 0), 15), ((3, 0), 2), ((2, 2), 3), ((10, 0), 23)])
 def test_chain_ofeat_matches_o_route(cuda, nspins, flux):
     N = sum(nspins)
     model = make_network(config.System(nspins=nspins, flux=flux), config.Network())
