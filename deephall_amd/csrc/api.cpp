@@ -476,6 +476,7 @@ int derive_weights(dh_handle* h, hipStream_t st) {
       launch_split_planes(h->l1w + nb, 32, d.D, 32, h->l1p + pb, st);
       h->p.L1BP = h->l1p;
       h->p.L1VP = h->l1p + pb;
+      h->p.L1VT = h->l1w + nb;
     }
   }
   if (d.D % 32 == 0) {
@@ -820,6 +821,13 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
         PROF(PK_GEMM + PK_CH, 2.0 * R * DD * DD, f4 * (3.0 * R * DD + DD * DD));
         launch_gemm_lnch(d.N, w.h, lp.WmP, x6_plane_rows(D), lp.bm, lp.ln2, w.geo, w.h, nw * d.N, 1, s);
       }
+      continue;
+    }
+    if (C > 1 && l == 0 && fused && ln_feat && P.L1VT && layer1_ch_supported(d)) {
+      // layer 1 at N = 10, 20 in one launch from the o~ rows (layernorm.hip layer1_ch_kernel:
+      // LN_ch1, Wm in coefficient space, tanh_ch, LN_ch2)
+      PROF(PK_L1CH, 2.0 * R * DD * (24.0 + 27.0), f4 * (R * KO + R * DD));
+      launch_layer1_ch(d, w.o, P.UT, P.L1VT, P.W0, lp.bol, lp.ln1, lp.ln2, w.geo, w.h, nw, s);
       continue;
     }
     // t = h + o (Wo Wl) + bo Wl    (psiformer.py:44-45, two adjacent linear maps folded);

@@ -51,8 +51,10 @@ struct Params {
   // U[8 h + a][n] = sum_d Wv~[a][h dh + d] Wol[h dh + d][n] (a < 5; a = 5..7 zero), and its planes
   const float* UT;
   const uint16_t* UP;
-  // layer 1 in coefficient space (gemm_lnch MODE 2, H = 4): planes of V^T and B^T [3][ldp][32]
+  // layer 1 in coefficient space (gemm_lnch MODE 2, H = 4): planes of V^T and B^T [3][ldp][32],
+  // and V^T [256][32] itself (layer1_ch_kernel, N = 10, 20)
   const uint16_t *L1VP, *L1BP;
+  const float* L1VT;
   const float* W2T;     // envelope first (env_first): W2T [256 2N][KE] and its planes
   const uint16_t* W2P;
 };
@@ -201,6 +203,12 @@ void launch_ofeat_weight(const Dims& d, const float* W0qkv, const float* bqkv, c
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
                       int nw, int C, int mode, hipStream_t s,
                       const float* W0f = nullptr);
+// layer 1 of the local energy at N = 10, 20 in one launch from the o~ rows O [ne C][KO]
+// (layernorm.hip layer1_ch_kernel): UT = U^T [256][KO], VT = V^T [256][32] (launch_l1_basis)
+bool layer1_ch_supported(const Dims& d);
+void launch_layer1_ch(const Dims& d, const float* O, const float* UT, const float* VT, const float* W0f,
+                      const float* bol, const float* ln1, const float* ln2, const float* geo, float* h, int nw,
+                      hipStream_t s);
 
 // det.hip
 //   value mode (C == 1): logpsi[nw][2]

@@ -443,6 +443,313 @@ __global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, 
         gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
 }
 
+// Layer 1 of the local energy at N = 10, 20 in ONE launch (round 6), from the o~ rows of
+// attention_feat2_kernel (psiformer.py:44-48 on the 2N+5 channel rows):
+//   h = LN_ch2(h1 + tanh_ch(h1 Wm + bm)),  h1 = LN_ch1(f W0 + o~ U + bol).
+// Four waves per electron as layernorm_ch_quad_kernel (lane = one feature column, all C channel
+// rows in registers, the same transposed sums):
+//   x_c = f_c . W0[:, col] + o~_c . U[:, col] (+ bol on the value row): 4 + 20 FMAs per row from
+//     the lane's columns of W0 / U and the electron's o~ rows (LDS, broadcast reads);
+//   LN_ch1 -> h1 (the quad kernel's statistics and output algebra);
+//   h1 Wm + bm in coefficient space (gemm_lnch.hip MODE 2): h1_c = r_c B with r_c LN_ch1's
+//     combination of the rows zh_c = (f_c, o~_c, [c = 0], -mean_c) and B = [E diag(gamma); beta],
+//     so h1_c Wm + bm = r_c V, V = B Wm (+ bm on the beta row; launch_l1_basis, f64 sums):
+//     27 FMAs per row from the lane's column of V instead of a 256-deep GEMM;
+//   tanh_ch, + h1, LN_ch2, h stored once.
+// It replaces the o~ U GEMM, two layernorm_ch_quad passes and the Wm GEMM: the o~ rows are read
+// (128 B per row) and h written (1 KB per row), nothing else goes through HBM.
+#ifndef L1CH_WPE  // A/B knobs of layer1_ch_kernel: waves per SIMD targeted, rows of LDS reads in flight
+#define L1CH_WPE 2
+#endif
+#ifndef L1CH_XDEP
+#define L1CH_XDEP 2
+#endif
+#ifndef L1CH_YDEP
+#define L1CH_YDEP 1
+#endif
+template <int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE))) void layer1_ch_kernel(const float* __restrict__ O, int KO,
+                                                        const float* __restrict__ UT, const float* __restrict__ VT,
+                                                        const float* __restrict__ W0f, const float* __restrict__ bol,
+                                                        const float* __restrict__ ln1, const float* __restrict__ ln2,
+                                                        const float* __restrict__ geo, float* __restrict__ h, int n_up) {
+  constexpr int T = 2 * N, C = 2 * N + 5, D = 256, NR = C + T + 3, NO = 20, NB = 27;
+  __shared__ float red[4][C + NR];
+  __shared__ float al[3][T];       // flow coefficients (broadcast reads)
+  __shared__ float tb[4][16 * 65];  // per-wave transpose scratch
+  __shared__ float mu[C], fin[NR], cf[T + 12];
+  __shared__ float4 os4[C * NO / 4];  // the electron's o~ rows, 5 slots per head (80-B rows)
+  __shared__ float zt[C * 28];        // the zh rows (f_c, o~_c, [c = 0], -mean_c, 0)
+  __shared__ float4 rr4[C * 7];       // LN_ch1's coefficient rows r_c (112-B rows, 27 used)
+  float* const os = reinterpret_cast<float*>(os4);
+  float* const rr = reinterpret_cast<float*>(rr4);
+  const int e = blockIdx.x;    // walker*N + electron
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = e / N, i = e - b * N, col = 64 * w + lane;
+  if (tid < N) {
+    const int q = tid;
+    const float4 g = *reinterpret_cast<const float4*>(geo + 4 * (size_t)(b * N + q));  // st ct sp cp
+    al[0][2 * q] = -g.z;
+    al[1][2 * q] = g.w;
+    al[2][2 * q] = 0.f;
+    al[0][2 * q + 1] = -(g.y * g.w);
+    al[1][2 * q + 1] = -(g.y * g.z);
+    al[2][2 * q + 1] = g.x;
+  }
+  for (int q = tid; q < C * NO; q += 256) {
+    const int c = q / NO, k = q - (q / NO) * NO;
+    os[q] = O[((size_t)e * C + c) * KO + 8 * (k / 5) + k % 5];
+  }
+  float w0[4], uc[NO];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w0[k] = W0f[k * D + col];
+#pragma unroll
+  for (int k = 0; k < NO; ++k) uc[k] = UT[(size_t)col * KO + 8 * (k / 5) + k % 5];
+  const float bo = bol[col];
+  const float4 g4 = *reinterpret_cast<const float4*>(geo + 4 * (size_t)e);  // st ct sp cp
+  // input.hip's channel seed f_c of this electron
+  auto feat = [&](int c) __attribute__((always_inline)) {
+    const float st = g4.x, ct = g4.y, sp = g4.z, cp = g4.w;
+    const float rx = st * cp, ry = st * sp, rz = ct;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c == 0) {
+      f = make_float4(rz, rx, ry, (i < n_up) ? 1.f : -1.f);
+    } else if (c <= T) {
+      const int t = c - 1;
+      if ((t >> 1) == i) f = ((t & 1) == 0) ? make_float4(-st, ct * cp, ct * sp, 0.f) : make_float4(0.f, -sp, cp, 0.f);
+    } else if (c == T + 1) {
+      f = make_float4(-2.f * rz, -2.f * rx, -2.f * ry, 0.f);
+    } else {
+      const int k = c - T - 2;  // 0:x 1:y 2:z
+      f = make_float4((k == 2) ? 0.f : -rz, (k == 0) ? 0.f : -rx, (k == 1) ? 0.f : -ry, 0.f);
+    }
+    return f;
+  };
+  __syncthreads();
+  // ---- x_c = (o~_c U + [c = 0] bol) + f_c W0 (the GEMM-then-residual order of the two-kernel form)
+  // (each row's offset passes through an opaque asm that also takes the row two back: left free,
+  // the scheduler issues every row's LDS reads ahead of the first use and spills)
+  float z[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    int off = c * (NO / 4);
+    if (c >= L1CH_XDEP)
+      asm volatile("" : "+s"(off) : "v"(z[c - L1CH_XDEP]));
+    else
+      asm volatile("" : "+s"(off));
+    float x = 0.f;
+#pragma unroll
+    for (int k4 = 0; k4 < NO / 4; ++k4) {  // broadcast ds_read_b128
+      const float4 o4 = os4[off + k4];
+      x = fmaf(o4.x, uc[4 * k4], x);
+      x = fmaf(o4.y, uc[4 * k4 + 1], x);
+      x = fmaf(o4.z, uc[4 * k4 + 2], x);
+      x = fmaf(o4.w, uc[4 * k4 + 3], x);
+    }
+    if (c == 0) x += bo;
+    const float4 f = feat(c);
+    z[c] = x + (f.x * w0[0] + f.y * w0[1] + f.z * w0[2] + f.w * w0[3]);
+  }
+  float* tw = tb[w];
+  // sums over this wave's 64 columns of R per-lane values getv(r) -> dst[r] (layernorm_ch_quad's)
+  auto rows_sum = [&](auto getv, auto R_, float* dst) {
+    constexpr int R = decltype(R_)::value;
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0 += 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (r0 + j < R) tw[j * 65 + lane] = getv(r0 + j);
+      __builtin_amdgcn_wave_barrier();
+      const int j = lane >> 2, q = lane & 3;
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v += tw[j * 65 + 16 * q + m];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      if (q == 0 && r0 + j < R) dst[r0 + j] = v;
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
+  // channel LayerNorm statistics of z (layernorm_ch_quad_kernel's): centres z, forms u, leaves the
+  // means in mu, the per-electron coefficients in cf; returns s
+  float u[3];
+  auto ln_stats = [&]() __attribute__((always_inline)) {
+    rows_sum([&](int c) { return z[c]; }, std::integral_constant<int, C>{}, red[w]);
+    __syncthreads();
+    if (tid < C) mu[tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) * (1.f / D);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < C; ++c) z[c] -= mu[c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      u[k] = 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) u[k] = fmaf(al[k][t], z[1 + t], u[k]);
+    }
+    rows_sum(
+        [&](int r) {
+          if (r < C) return z[0] * z[r];
+          if (r < C + T) return z[1 + r - C] * z[1 + r - C];
+          return u[r - C - T] * u[r - C - T];
+        },
+        std::integral_constant<int, NR>{}, red[w] + C);
+    __syncthreads();
+    for (int r = tid; r < NR; r += 256)
+      fin[r] = ((red[0][C + r] + red[1][C + r]) + (red[2][C + r] + red[3][C + r])) * (1.f / D);
+    __syncthreads();
+    const float s = 1.f / sqrtf(fin[0] + 1e-5f), s2 = s * s;
+    if (w == 0) {
+      float clv = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      if (lane < T) {
+        const float at = s2 * fin[1 + lane];
+        cf[lane] = at;
+        clv = 3.f * at * at - s2 * fin[C + lane];
+        a0 = al[0][lane] * at;
+        a1 = al[1][lane] * at;
+        a2 = al[2][lane] * at;
+      }
+      clv = wave_sum(clv);
+      a0 = wave_sum(a0);
+      a1 = wave_sum(a1);
+      a2 = wave_sum(a2);
+      if (lane == 0) {
+        cf[T] = clv;
+        cf[T + 1] = s2 * fin[1 + T];  // aL
+        const float au[3] = {a0, a1, a2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          cf[T + 2 + k] = au[k];
+          cf[T + 5 + k] = 3.f * au[k] * au[k] - s2 * fin[C + T + k];
+          cf[T + 8 + k] = s2 * fin[2 + T + k];  // aS_k
+        }
+      }
+    }
+    __syncthreads();
+    return s;
+  };
+  // ---- LN_ch1 -> h1 (in z)
+  float s = ln_stats();
+  {
+    const float g = ln1[col], bb = ln1[D + col], gs = g * s, z0 = z[0];
+    float sat = 0.f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float at = cf[t];
+      sat = fmaf(at, z[1 + t], sat);
+      z[1 + t] = gs * (z[1 + t] - at * z0);
+    }
+    z[1 + T] = gs * (z[1 + T] - cf[T + 1] * z0 - 2.f * sat + cf[T] * z0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) z[2 + T + k] = gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
+    z[0] = g * (s * z0) + bb;
+  }
+  // ---- r rows: LN_ch1's combinations of the zh rows (zh staged in LDS first, one element per
+  // task; then the tangent rows one element per task, the L / flow rows by thread j < 27)
+#pragma unroll 1
+  for (int q = tid; q < C * 28; q += 256) {
+    const int c = q / 28, j = q - (q / 28) * 28;
+    float v = 0.f;
+    if (j < 4) {
+      const float4 f = feat(c);
+      v = j == 0 ? f.x : (j == 1 ? f.y : (j == 2 ? f.z : f.w));
+    } else if (j < 24) {
+      v = os[c * NO + j - 4];
+    } else if (j == 24) {
+      v = c == 0 ? 1.f : 0.f;
+    } else if (j == 25) {
+      v = -mu[c];
+    }
+    zt[q] = v;  // j = 26: the beta row (zh has 0 there), j = 27: padding
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int q = tid; q < T * 28; q += 256) {
+    const int t = q / 28, j = q - (q / 28) * 28;
+    rr[(1 + t) * 28 + j] = s * (zt[(1 + t) * 28 + j] - cf[t] * zt[j]);
+  }
+  if (tid < NB) {
+    const int j = tid;
+    const float zh0 = zt[j];
+    rr[j] = j == 26 ? 1.f : s * zh0;
+    float sat = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) {
+      const float zv = zt[(1 + t) * 28 + j];
+      sat = fmaf(cf[t], zv, sat);
+      u0 = fmaf(al[0][t], zv, u0);
+      u1 = fmaf(al[1][t], zv, u1);
+      u2 = fmaf(al[2][t], zv, u2);
+    }
+    rr[(1 + T) * 28 + j] = s * (zt[(1 + T) * 28 + j] - cf[T + 1] * zh0 - 2.f * sat + cf[T] * zh0);
+    const float uk[3] = {u0, u1, u2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      rr[(2 + T + k) * 28 + j] =
+          s * (zt[(2 + T + k) * 28 + j] - cf[T + 8 + k] * zh0 - 2.f * cf[T + 2 + k] * uk[k] + cf[T + 5 + k] * zh0);
+  }
+  __syncthreads();
+  // ---- y = h1 Wm + bm = r V, tanh_ch, + h1 (layernorm_ch_quad mode 1's order)
+  {
+    // V's column, requested here (an opaque base: hoisted to the kernel start, its 27 registers
+    // would be live through LN_ch1)
+    const float* vt = VT + (size_t)col * 32;
+    asm volatile("" : "+v"(vt));
+    float v[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) v[j] = vt[j];
+    float prev = 0.f, prev2 = 0.f;  // the previous rows' results (order the rows' LDS reads, as above)
+    auto yrow = [&](int c) __attribute__((always_inline)) {
+      int off = c * 7;
+      asm volatile("" : "+s"(off) : "v"(L1CH_YDEP == 1 ? prev : prev2));
+      float a = 0.f;
+#pragma unroll
+      for (int j4 = 0; j4 < 7; ++j4) {  // broadcast ds_read_b128 (r[27] = 0 pads the last)
+        const float4 r4 = rr4[off + j4];
+        a = fmaf(r4.x, v[4 * j4], a);
+        a = fmaf(r4.y, v[4 * j4 + 1], a);
+        a = fmaf(r4.z, v[4 * j4 + 2], a);
+        if (4 * j4 + 3 < NB) a = fmaf(r4.w, v[4 * j4 + 3], a);
+      }
+      prev2 = prev;
+      prev = a;
+      return a;
+    };
+    const float y0 = tanhf(yrow(0)), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
+    float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+    z[0] = z[0] + y0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float yt = yrow(1 + t);
+      sq = fmaf(yt, yt, sq);
+      u0 = fmaf(al[0][t], yt, u0);
+      u1 = fmaf(al[1][t], yt, u1);
+      u2 = fmaf(al[2][t], yt, u2);
+      z[1 + t] = fmaf(d1, yt, z[1 + t]);
+    }
+    z[1 + T] = z[1 + T] + d1 * yrow(1 + T) + d2 * sq;
+    const float uu[3] = {u0, u1, u2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) z[2 + T + k] = z[2 + T + k] + d1 * yrow(2 + T + k) + d2 * uu[k] * uu[k];
+  }
+  // ---- LN_ch2 -> h
+  s = ln_stats();
+  const size_t r0 = (size_t)e * C * D + col;
+  const float g = ln2[col], bb = ln2[D + col], gs = g * s, z0 = z[0];
+  float sat = 0.f;
+  h[r0] = g * (s * z0) + bb;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const float at = cf[t];
+    sat = fmaf(at, z[1 + t], sat);
+    h[r0 + (size_t)(1 + t) * D] = gs * (z[1 + t] - at * z0);
+  }
+  h[r0 + (size_t)(1 + T) * D] = gs * (z[1 + T] - cf[T + 1] * z0 - 2.f * sat + cf[T] * z0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    h[r0 + (size_t)(2 + T + k) * D] =
+        gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
+}
+
 template <int N>
 void launch_ln_wave(const float* X, const float* Z, const float* ln, const float* geo, float* h, int ne, int mode,
                     hipStream_t s) {
@@ -450,6 +757,20 @@ void launch_ln_wave(const float* X, const float* Z, const float* ln, const float
 }
 
 }  // namespace
+
+bool layer1_ch_supported(const Dims& d) { return d.D == 256 && d.H == 4 && ofeat_k(d) == 32 && (d.N == 10 || d.N == 20); }
+
+void launch_layer1_ch(const Dims& d, const float* O, const float* UT, const float* VT, const float* W0f,
+                      const float* bol, const float* ln1, const float* ln2, const float* geo, float* h, int nw,
+                      hipStream_t s) {
+  const int ne = nw * d.N, KO = ofeat_k(d);
+  if (d.N == 10)
+    hipLaunchKernelGGL(layer1_ch_kernel<10>, dim3(ne), dim3(256), 0, s, O, KO, UT, VT, W0f, bol, ln1, ln2, geo, h,
+                       d.n_up);
+  else  // layer1_ch_supported: N = 10 or 20
+    hipLaunchKernelGGL(layer1_ch_kernel<20>, dim3(ne), dim3(256), 0, s, O, KO, UT, VT, W0f, bol, ln1, ln2, geo, h,
+                       d.n_up);
+}
 
 void launch_layernorm(const Dims& d, const float* X, const float* Z, const float* ln, const float* geo, float* h,
                       int nw, int C, int mode, hipStream_t s, const float* W0f) {
