@@ -728,7 +728,13 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // Its 96-row tiles suit up to ~64K walker rows (C2 24576: 256 tiles, C4 40960: 427); at
   // C5 (81920 rows, 2320 orbital columns) the separate GEMMs with 128-row LayerNorm tiles are
   // faster (102.6 vs 103.6 ms per step, tools/chain_bench.py, profiles/)
-  const bool chain = C == 1 && x6 && ln_fused && D == 256 && rows < 65536;
+  // Past 64K rows at N = 20 (C5) layer 1 still takes the chain, its attention in the prologue:
+  // the layer's attention, two LayerNorm GEMMs and layer 2's q|k|v in one launch (round 6)
+  const bool chain_any = C == 1 && x6 && ln_fused && D == 256;
+  auto chain_at = [&](int l) {
+    return chain_any && (rows < 65536 || (l == 0 && d.N >= 20 && attention_takes_features(d, C) && d.L > 0 &&
+                                          chain_attn_supported(d.N, d.H, d.dh)));
+  };
   // local energy, split-bf16, D = 256, N <= 8: GEMM + channel LayerNorm fused per map
   const bool lnch = C > 1 && x6 && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&
                     gemm_lnch_supported(d.N, D);
@@ -748,7 +754,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   }
   for (int l = 0; l < d.L; ++l) {
     const LayerParams& lp = P.layer[l];
-    if (l > 0 && !chain)
+    const bool chain = chain_at(l);
+    if (l > 0 && !chain_at(l - 1))  // (a chained layer's last pass wrote this layer's q|k|v)
       gemm(w.h, D, lp.Wqkv, lp.WqkvT, lp.WqkvP, 3 * D, lp.bqkv, nullptr, 0, w.qkv, 3 * D, 3 * D, D);
     // log psi, chain form: layer 1's attention runs in the chain kernel's prologue (its o
     // never leaves the CU; attn_val.h)
@@ -848,7 +855,7 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
     }
   }
   // (the envelope-first local energy maps only six special rows per electron, det.hip)
-  if ((!chain || d.L == 0) && !(C > 1 && env_first(d)))
+  if ((d.L == 0 || !chain_at(d.L - 1)) && !(C > 1 && env_first(d)))
     gemm(w.h, D, P.Worb, P.WorbT, P.WorbP, d.ld_orb, P.borb, nullptr, 0, w.F, d.ld_orb, d.orb_cols, D);
   return check_launch();
 }

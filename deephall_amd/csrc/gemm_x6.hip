@@ -2986,7 +2986,8 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
       case 4: k = chain_x6s_kernel<4>; break;
       case 6: k = chain_x6s_kernel<6>; break;
       case 8: k = chain_x6s_kernel<8>; break;
-      default: k = chain_x6s_kernel<10>; break;
+      case 10: k = chain_x6s_kernel<10>; break;
+      default: k = chain_x6s_kernel<20>; break;
     }
   }
   const int trw = feat.W0qkv ? (CH_BM / feat.N) * feat.N : CH_BM;  // the kernel's TRW
@@ -2997,7 +2998,7 @@ void launch_chain_x6(const float* X1, const uint16_t* Wp1, int ldp1, const float
 // Layer 1's attention inside the chain prologue (chain_x6s_kernel<N>): walker-aligned 96-row
 // tiles, 4 heads of 64 (one per wave pair)
 bool chain_attn_supported(int N, int H, int dh) {
-  return H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8 || N == 10);
+  return H == 4 && dh == 64 && (N == 2 || N == 3 || N == 4 || N == 6 || N == 8 || N == 10 || N == 20);
 }
 
 }  // namespace dh
