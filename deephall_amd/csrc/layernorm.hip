@@ -467,6 +467,9 @@ __global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, 
 #ifndef L1CH_YDEP
 #define L1CH_YDEP 1
 #endif
+#ifndef L1CH_ABL  // ablation builds (tools only, wrong results): bit 0 no x, 1 no LN_ch1, 2 no r rows / y, 3 no LN_ch2
+#define L1CH_ABL 0
+#endif
 template <int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE))) void layer1_ch_kernel(const float* __restrict__ O, int KO,
                                                         const float* __restrict__ UT, const float* __restrict__ VT,
@@ -526,6 +529,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     return f;
   };
   __syncthreads();
+#if L1CH_ABL & 1
+  float z[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) z[c] = uc[c % NO] * (float)(c + 1);
+#else
   // ---- x_c = (o~_c U + [c = 0] bol) + f_c W0 (the GEMM-then-residual order of the two-kernel form)
   // (each row's offset passes through an opaque asm that also takes the row two back: left free,
   // the scheduler issues every row's LDS reads ahead of the first use and spills)
@@ -550,6 +558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     const float4 f = feat(c);
     z[c] = x + (f.x * w0[0] + f.y * w0[1] + f.z * w0[2] + f.w * w0[3]);
   }
+#endif
   float* tw = tb[w];
   // sums over this wave's 64 columns of R per-lane values getv(r) -> dst[r] (layernorm_ch_quad's)
   auto rows_sum = [&](auto getv, auto R_, float* dst) {
@@ -628,7 +637,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     return s;
   };
   // ---- LN_ch1 -> h1 (in z)
+#if L1CH_ABL & 2  // (ablation builds only: wrong results)
+  float s = 1.f;
+  u[0] = u[1] = u[2] = 0.f;
+#else
   float s = ln_stats();
+#endif
   {
     const float g = ln1[col], bb = ln1[D + col], gs = g * s, z0 = z[0];
     float sat = 0.f;
@@ -643,8 +657,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     for (int k = 0; k < 3; ++k) z[2 + T + k] = gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
     z[0] = g * (s * z0) + bb;
   }
+  // V's column, requested here, ahead of the r rows (an opaque base: hoisted to the kernel start,
+  // its 27 registers would be live through LN_ch1)
+  const float* vt = VT + (size_t)col * 32;
+  asm volatile("" : "+v"(vt));
+  float v[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) v[j] = vt[j];
+#if !(L1CH_ABL & 4)
   // ---- r rows: LN_ch1's combinations of the zh rows (zh staged in LDS first, one element per
-  // task; then the tangent rows one element per task, the L / flow rows by thread j < 27)
+  // task; then the tangent rows one element per task, the L / flow rows below)
 #pragma unroll 1
   for (int q = tid; q < C * 28; q += 256) {
     const int c = q / 28, j = q - (q / 28) * 28;
@@ -667,36 +689,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     const int t = q / 28, j = q - (q / 28) * 28;
     rr[(1 + t) * 28 + j] = s * (zt[(1 + t) * 28 + j] - cf[t] * zt[j]);
   }
-  if (tid < NB) {
-    const int j = tid;
-    const float zh0 = zt[j];
-    rr[j] = j == 26 ? 1.f : s * zh0;
-    float sat = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
-#pragma unroll 1
-    for (int t = 0; t < T; ++t) {
-      const float zv = zt[(1 + t) * 28 + j];
-      sat = fmaf(cf[t], zv, sat);
-      u0 = fmaf(al[0][t], zv, u0);
-      u1 = fmaf(al[1][t], zv, u1);
-      u2 = fmaf(al[2][t], zv, u2);
-    }
-    rr[(1 + T) * 28 + j] = s * (zt[(1 + T) * 28 + j] - cf[T + 1] * zh0 - 2.f * sat + cf[T] * zh0);
-    const float uk[3] = {u0, u1, u2};
+  // the L / flow rows: their sums over t split over the four waves (lanes j < 27 of wave w take
+  // t = w T / 4 ..), the partials combined in a fixed order
+  {
+    __shared__ float part4[4][4][28];
+    constexpr int TQ = T / 4;
+    static_assert(T % 4 == 0, "t split over four waves");
+    if (lane < NB) {
+      const int j = lane;
+      float sat = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-      rr[(2 + T + k) * 28 + j] =
-          s * (zt[(2 + T + k) * 28 + j] - cf[T + 8 + k] * zh0 - 2.f * cf[T + 2 + k] * uk[k] + cf[T + 5 + k] * zh0);
+      for (int tt = 0; tt < TQ; ++tt) {
+        const int t = w * TQ + tt;
+        const float zv = zt[(1 + t) * 28 + j];
+        sat = fmaf(cf[t], zv, sat);
+        u0 = fmaf(al[0][t], zv, u0);
+        u1 = fmaf(al[1][t], zv, u1);
+        u2 = fmaf(al[2][t], zv, u2);
+      }
+      part4[w][0][j] = sat;
+      part4[w][1][j] = u0;
+      part4[w][2][j] = u1;
+      part4[w][3][j] = u2;
+    }
+    __syncthreads();
+    if (tid < NB) {
+      const int j = tid;
+      const float zh0 = zt[j];
+      rr[j] = j == 26 ? 1.f : s * zh0;
+      float a4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a4[q] = (part4[0][q][j] + part4[1][q][j]) + (part4[2][q][j] + part4[3][q][j]);
+      rr[(1 + T) * 28 + j] = s * (zt[(1 + T) * 28 + j] - cf[T + 1] * zh0 - 2.f * a4[0] + cf[T] * zh0);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        rr[(2 + T + k) * 28 + j] =
+            s * (zt[(2 + T + k) * 28 + j] - cf[T + 8 + k] * zh0 - 2.f * cf[T + 2 + k] * a4[1 + k] + cf[T + 5 + k] * zh0);
+    }
   }
   __syncthreads();
+#endif
+#if !(L1CH_ABL & 4)
   // ---- y = h1 Wm + bm = r V, tanh_ch, + h1 (layernorm_ch_quad mode 1's order)
   {
-    // V's column, requested here (an opaque base: hoisted to the kernel start, its 27 registers
-    // would be live through LN_ch1)
-    const float* vt = VT + (size_t)col * 32;
-    asm volatile("" : "+v"(vt));
-    float v[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) v[j] = vt[j];
     float prev = 0.f, prev2 = 0.f;  // the previous rows' results (order the rows' LDS reads, as above)
     auto yrow = [&](int c) __attribute__((always_inline)) {
       int off = c * 7;
@@ -731,8 +766,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
 #pragma unroll
     for (int k = 0; k < 3; ++k) z[2 + T + k] = z[2 + T + k] + d1 * yrow(2 + T + k) + d2 * uu[k] * uu[k];
   }
+#endif
   // ---- LN_ch2 -> h
+#if !(L1CH_ABL & 8)
   s = ln_stats();
+#endif
   const size_t r0 = (size_t)e * C * D + col;
   const float g = ln2[col], bb = ln2[D + col], gs = g * s, z0 = z[0];
   float sat = 0.f;
