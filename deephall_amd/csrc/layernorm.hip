@@ -467,6 +467,9 @@ __global__ __launch_bounds__(256) void layernorm_ch_quad_kernel(const float* X, 
 #ifndef L1CH_YDEP
 #define L1CH_YDEP 1
 #endif
+#ifndef L1CH_MFMA  // A/B knob: layer1_ch_kernel's r V product on the matrix cores (else VALU FMAs on broadcast reads)
+#define L1CH_MFMA 1
+#endif
 #ifndef L1CH_ABL  // ablation builds (tools only, wrong results): bit 0 no x, 1 no LN_ch1, 2 no r rows / y, 3 no LN_ch2
 #define L1CH_ABL 0
 #endif
@@ -479,13 +482,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
   constexpr int T = 2 * N, C = 2 * N + 5, D = 256, NR = C + T + 3, NO = 20, NB = 27;
   __shared__ float red[4][C + NR];
   __shared__ float al[3][T];       // flow coefficients (broadcast reads)
-  __shared__ float tb[4][16 * 65];  // per-wave transpose scratch
   __shared__ float mu[C], fin[NR], cf[T + 12];
-  __shared__ float4 os4[C * NO / 4];  // the electron's o~ rows, 5 slots per head (80-B rows)
-  __shared__ float zt[C * 28];        // the zh rows (f_c, o~_c, [c = 0], -mean_c, 0)
-  __shared__ float4 rr4[C * 7];       // LN_ch1's coefficient rows r_c (112-B rows, 27 used)
-  float* const os = reinterpret_cast<float*>(os4);
+  __shared__ float4 rr4[C * 7];    // LN_ch1's coefficient rows r_c (112-B rows, 27 used + 0 pad)
   float* const rr = reinterpret_cast<float*>(rr4);
+  // one pool: the per-wave transpose scratch tb [4][16 * 65], the zh rows zt [C][28] (f_c, o~_c,
+  // [c = 0], -mean_c, 0), the o~ rows os [C][20]; overlaid by ys [C][256] (the MFMA form's y,
+  // between the r rows and LN_ch2, barriers on both sides)
+  constexpr int TBF = 4 * 16 * 65, POOL = (C * D > TBF + C * 28 + C * NO) ? C * D : TBF + C * 28 + C * NO;
+  __shared__ float4 pool4[POOL / 4];
+  float* const pool = reinterpret_cast<float*>(pool4);
+  float* const zt = pool + TBF;
+  float* const os = zt + C * 28;
+  const float4* const os4 = reinterpret_cast<const float4*>(os);
   const int e = blockIdx.x;    // walker*N + electron
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b = e / N, i = e - b * N, col = 64 * w + lane;
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     z[c] = x + (f.x * w0[0] + f.y * w0[1] + f.z * w0[2] + f.w * w0[3]);
   }
 #endif
-  float* tw = tb[w];
+  float* tw = pool + w * 16 * 65;
   // sums over this wave's 64 columns of R per-lane values getv(r) -> dst[r] (layernorm_ch_quad's)
   auto rows_sum = [&](auto getv, auto R_, float* dst) {
     constexpr int R = decltype(R_)::value;
@@ -657,6 +665,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
     for (int k = 0; k < 3; ++k) z[2 + T + k] = gs * (z[2 + T + k] - cf[T + 8 + k] * z0 - 2.f * cf[T + 2 + k] * u[k] + cf[T + 5 + k] * z0);
     z[0] = g * (s * z0) + bb;
   }
+#if L1CH_MFMA
+  // V^T fragments of this wave's 4 feature tiles (the MFMA A operand, requested ahead of the r
+  // rows): lane (i, kq) holds V[4 ks + kq][64 w + 16 ft + i]
+  const int li = lane & 15, kq = lane >> 4;
+  const float* vt = VT + (size_t)(64 * w + li) * 32 + kq;
+  asm volatile("" : "+v"(vt));
+  float va[4][7];
+#pragma unroll
+  for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) va[ft][ks] = vt[ft * 16 * 32 + 4 * ks];
+#else
   // V's column, requested here, ahead of the r rows (an opaque base: hoisted to the kernel start,
   // its 27 registers would be live through LN_ch1)
   const float* vt = VT + (size_t)col * 32;
@@ -664,6 +684,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
   float v[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) v[j] = vt[j];
+#endif
 #if !(L1CH_ABL & 4)
   // ---- r rows: LN_ch1's combinations of the zh rows (zh staged in LDS first, one element per
   // task; then the tangent rows one element per task, the L / flow rows below)
@@ -713,6 +734,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
       part4[w][3][j] = u2;
     }
     __syncthreads();
+    if (tid == NB) {  // the pad column (k = 27 of the MFMA form) of the rows written below
+      rr[NB] = 0.f;
+      rr[(1 + T) * 28 + NB] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) rr[(2 + T + k) * 28 + NB] = 0.f;
+    }
     if (tid < NB) {
       const int j = tid;
       const float zh0 = zt[j];
@@ -731,6 +758,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
 #endif
 #if !(L1CH_ABL & 4)
   // ---- y = h1 Wm + bm = r V, tanh_ch, + h1 (layernorm_ch_quad mode 1's order)
+#if L1CH_MFMA
+  // y^T = V^T r^T on the matrix cores (v_mfma_f32_16x16x4_f32, exact f32): wave w takes features
+  // 64 w .. 64 w + 63 (4 tiles of 16) x all channels (CT tiles of 16), K = 28 (r's 27 terms and
+  // the zero pad); the result goes through LDS (ys [C][256]) into the lane-per-feature layout
+  float* const ys = pool;
+  {
+    constexpr int CT = (C + 15) / 16;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v acc[4][CT];
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[ft][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 7; ++ks) {
+      float rb[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int ch = 16 * ct + li;
+        rb[ct] = ch < C ? rr[ch * 28 + 4 * ks + kq] : 0.f;
+      }
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[ft][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[ft][ks], rb[ct], acc[ft][ct], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int ch = 16 * ct + li;
+        if (ch < C)
+          *reinterpret_cast<float4*>(&ys[ch * D + 64 * w + 16 * ft + 4 * kq]) =
+              make_float4(acc[ft][ct][0], acc[ft][ct][1], acc[ft][ct][2], acc[ft][ct][3]);
+      }
+  }
+  __syncthreads();
+  {
+    auto yrow = [&](int c) __attribute__((always_inline)) { return ys[c * D + col]; };
+#else
   {
     float prev = 0.f, prev2 = 0.f;  // the previous rows' results (order the rows' LDS reads, as above)
     auto yrow = [&](int c) __attribute__((always_inline)) {
@@ -749,6 +816,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
       prev = a;
       return a;
     };
+#endif
     const float y0 = tanhf(yrow(0)), d1 = 1.f - y0 * y0, d2 = -2.f * y0 * d1;
     float sq = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
     z[0] = z[0] + y0;
@@ -766,6 +834,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L1CH_WPE)))
 #pragma unroll
     for (int k = 0; k < 3; ++k) z[2 + T + k] = z[2 + T + k] + d1 * yrow(2 + T + k) + d2 * uu[k] * uu[k];
   }
+#if L1CH_MFMA
+  __syncthreads();  // every ys read done: LN_ch2's transposes reuse the pool
+#endif
 #endif
   // ---- LN_ch2 -> h
 #if !(L1CH_ABL & 8)
