@@ -830,7 +830,8 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
       }
       continue;
     }
-    if (C > 1 && l == 0 && fused && ln_feat && P.L1VT && layer1_ch_supported(d)) {
+    if (C > 1 && l == 0 && fused && ln_feat && P.L1VT && layer1_ch_supported(d) &&
+        h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED) {  // (the unfused mode keeps the two-kernel form: tests)
       // layer 1 at N = 10, 20 in one launch from the o~ rows (layernorm.hip layer1_ch_kernel:
       // LN_ch1, Wm in coefficient space, tanh_ch, LN_ch2)
       PROF(PK_L1CH, 2.0 * R * DD * (24.0 + 27.0), f4 * (R * KO + R * DD));

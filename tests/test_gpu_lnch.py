@@ -14,7 +14,10 @@ path against the float64 oracle is tests/test_gpu_floor.py and tests/test_gpu_pa
 which run in the default (fused) mode.
 
 Cases: N = 1, 2, 3 (C1), 5 (mixed spins), 6 (C2); batches whose electron count is not a
-multiple of the 16-electron tile (a partial last tile); C2 at the bench batch (4096).
+multiple of the 16-electron tile (a partial last tile); C2 at the bench batch (4096).  At N = 10
+and 20 (C4, C5; round 6) the fused form is layer 1 in one launch (layernorm.hip
+layer1_ch_kernel: LN_ch1, Wm in coefficient space on the matrix cores, tanh_ch, LN_ch2) and the
+two-pass form its o~ U GEMM + layernorm_ch_quad + Wm GEMM + layernorm_ch_quad.
 """
 
 from __future__ import annotations
@@ -38,6 +41,8 @@ CASES = [
     ("N5mix", dict(nspins=(3, 2), flux=6), 21),
     ("C2", dict(nspins=(6, 0), flux=15), 43),
     ("C2_bench", dict(nspins=(6, 0), flux=15), 4096),
+    ("C4", dict(nspins=(10, 0), flux=23), 24),
+    ("C5", dict(nspins=(20, 0), flux=57), 12),
 ]
 OBS = ["kinetic", "potential", "angular_momentum_z", "angular_momentum_z_square", "angular_momentum_square"]
 
