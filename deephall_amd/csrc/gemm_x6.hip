@@ -50,6 +50,9 @@
 #ifndef CHAIN_LBAR  // A/B knob: the chain kernel's barriers wait for LDS only (lgkmcnt(0) + s_barrier) instead
 #define CHAIN_LBAR 1  // of __syncthreads' vmcnt(0), which also waited for the next GEMM's weight prefetch (round 5)
 #endif
+#ifndef X6M_NT  // A/B knob: gemm_x6m's output tiles stored nontemporal (streaming) instead of plain stores
+#define X6M_NT 0
+#endif
 #ifndef CHAIN_STAMP  // diagnostic builds only (tools/chain_stamp.py): per-tile phase stamps of chain_x6s
 #define CHAIN_STAMP 0
 #endif
@@ -1848,7 +1851,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x6m_kernel(const float* __restric
             c[2] += rv[rb].z;
             c[3] += rv[rb].w;
           }
-          if (!(ABL & 4) || c[0] == 1.2345e-30f) *reinterpret_cast<f32x4*>(Y + (size_t)(rw0 + rb * 16 + l16) * ldy + n) = c;
+          if (!(ABL & 4) || c[0] == 1.2345e-30f) {
+            f32x4* yp = reinterpret_cast<f32x4*>(Y + (size_t)(rw0 + rb * 16 + l16) * ldy + n);
+            if constexpr (X6M_NT)
+              __builtin_nontemporal_store(c, yp);  // streaming: the weights stay resident in L2
+            else
+              *yp = c;
+          }
         }
       }
 #pragma unroll
