@@ -87,8 +87,14 @@ __device__ __forceinline__ void mbar() {
 #endif
 }
 
+#ifndef AMF_WPE10  // waves per SIMD targeted at N <= 10 / N = 20 (0 = the compiler's choice; 4 at N = 10: 128 VGPRs, no spill, r06 v30)
+#define AMF_WPE10 4
+#endif
+#ifndef AMF_WPE20
+#define AMF_WPE20 0
+#endif
 template <int N, bool FEAT>
-__global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ qkv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N <= 10 ? (AMF_WPE10 ? AMF_WPE10 : 1) : (AMF_WPE20 ? AMF_WPE20 : 1)))) void attention_mfma_kernel(const float* __restrict__ qkv,
                                                              const float* __restrict__ geo, float* __restrict__ o,
                                                              int H, const float* __restrict__ W0qkv,
                                                              const float* __restrict__ bqkv, int n_up) {
