@@ -728,12 +728,14 @@ int run_trunk(dh_handle* h, const float* x, int nw, int C, const Work& w, hipStr
   // Its 96-row tiles suit up to ~64K walker rows (C2 24576: 256 tiles, C4 40960: 427); at
   // C5 (81920 rows, 2320 orbital columns) the separate GEMMs with 128-row LayerNorm tiles are
   // faster (102.6 vs 103.6 ms per step, tools/chain_bench.py, profiles/)
-  // Past 64K rows at N = 20 (C5) layer 1 still takes the chain, its attention in the prologue:
-  // the layer's attention, two LayerNorm GEMMs and layer 2's q|k|v in one launch (round 6)
+  // At N = 20 (C5) the chain is taken past 64K rows too (round 6): layer 1 with its attention in
+  // the prologue (attention, two LayerNorm GEMMs and layer 2's q|k|v in one launch), layer 2 with
+  // the 2320-column orbital map as its last pass (C5 73.5 -> 74.2 K E_L/s, 2.53 -> 2.59 M
+  // walker-steps/s same box, profiles/r06_v35_chain_big20_ab.txt)
   const bool chain_any = C == 1 && x6 && ln_fused && D == 256;
   auto chain_at = [&](int l) {
-    return chain_any && (rows < 65536 || (l == 0 && d.N >= 20 && attention_takes_features(d, C) && d.L > 0 &&
-                                          chain_attn_supported(d.N, d.H, d.dh)));
+    (void)l;
+    return chain_any && (rows < 65536 || d.N >= 20);
   };
   // local energy, split-bf16, D = 256, N <= 8: GEMM + channel LayerNorm fused per map
   const bool lnch = C > 1 && x6 && C == 2 * d.N + 5 && h->gemm_mode != DH_GEMM_X6_ALL_UNFUSED &&

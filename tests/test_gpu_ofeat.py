@@ -9,9 +9,9 @@ attention_val_kernel) and contracts it with Wol.  Both routes must agree to f32 
 same walkers (distribution of the relative difference: median, p99, max): the first 1000
 walkers of a batch past 65536 rows (the o route) against the same 1000 walkers alone (the o~
 route, with a partial last tile), for N = 6 (C2), N = 3, the two-spin N = 4 and N = 10 (C4:
-90-row tiles of 9 whole walkers); at N = 20 (C5) both batches take the o~ route in layer 1 and
-the comparison pins the past-64K-rows form (layer 1 chained, layer 2 on separate GEMMs) against
-the all-chain form of the small batch; and the local energy of the o~ route against the float64 oracle lives in
+90-row tiles of 9 whole walkers); at N = 20 (C5) every batch size runs the chain (80-row layer-1
+tiles of 4 walkers, 96-row layer-2 tiles with the orbital map), so the big batch must reproduce
+the small one; and the local energy of the o~ route against the float64 oracle lives in
 test_gpu_parity.py / test_gpu_floor.py."""
 
 from __future__ import annotations
@@ -32,8 +32,7 @@ def test_chain_ofeat_matches_o_route(cuda, nspins, flux):
     N = sum(nspins)
     model = make_network(config.System(nspins=nspins, flux=flux), config.Network())
     params = model.init(PRNGKey(11), device=cuda)
-    # rows = big * N >= 65536: the non-chain log-psi path (at N = 20 layer 1 stays in the chain
-    # there, its 80-row tiles then run next to layer 2's separate GEMMs: the C5 bench's path)
+    # rows = big * N >= 65536: the non-chain log-psi path (at N = 20 the chain at any size)
     big = 65536 // N + 64
     x = init_guess(Key(5), big, N, cuda, network=model)
     lp_big = model.apply(params, x)[:1000].cpu().numpy()
